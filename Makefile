@@ -1,0 +1,41 @@
+# Build for MI355X (gfx950) only.  Outputs stay in-tree so they travel to the GPU box.
+#   make          -> qec_ldpc_amd/libqecldpc.so, oracle/liboracle.so, tools/qec_ldpc (CLI)
+HIPCC    ?= /opt/rocm/bin/hipcc
+ARCH     ?= gfx950
+# IEEE fp32 exactly as written: no contraction, no fast-math, denormals preserved.
+HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -Wall -Wno-unused-function
+CSRC     := qec_ldpc_amd/csrc
+OBJ      := build/obj
+LIB      := qec_ldpc_amd/libqecldpc.so
+OBJS     := $(OBJ)/bp_decode.o $(OBJ)/code_model.o $(OBJ)/capi.o
+HDRS     := include/qec_ldpc.h include/HostDeviceArray.h $(CSRC)/qec_internal.h
+
+all: $(LIB) oracle tools/qec_ldpc
+
+$(OBJ):
+	mkdir -p $(OBJ)
+
+$(OBJ)/bp_decode.o: $(CSRC)/bp_decode.hip $(HDRS) | $(OBJ)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(OBJ)/code_model.o: $(CSRC)/code_model.cpp $(HDRS) | $(OBJ)
+	$(HIPCC) $(HIPFLAGS) -x c++ -c $< -o $@
+
+$(OBJ)/capi.o: $(CSRC)/capi.cpp $(HDRS) | $(OBJ)
+	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
+
+$(LIB): $(OBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS) -Wl,--no-undefined
+
+# main.cu's Monte-Carlo driver on the GPU engine (caller side, tools/qec_ldpc_main.cpp)
+tools/qec_ldpc: tools/qec_ldpc_main.cpp include/*.h $(LIB)
+	$(HIPCC) -O2 -std=c++17 -Iinclude -o $@ $< -Lqec_ldpc_amd -lqecldpc -Wl,-rpath,'$$ORIGIN/../qec_ldpc_amd'
+
+oracle:
+	$(MAKE) -s -C oracle
+
+clean:
+	rm -rf build $(LIB) tools/qec_ldpc
+	$(MAKE) -s -C oracle clean
+
+.PHONY: all oracle clean

@@ -1,0 +1,150 @@
+/*
+ * qec_ldpc.h -- C ABI of libqecldpc.so, the MI355X (gfx950) belief-propagation
+ * decoder for quasi-cyclic CSS quantum LDPC codes.
+ *
+ * Plain C: opaque handles, plain pointers and sizes, int status codes
+ * (0 = ok, < 0 = error, text in qec_last_error()).  No HIP or torch types
+ * appear in any signature; streams are passed as `void*` (a hipStream_t or NULL).
+ *
+ * Each entry point names the reference interface it replaces
+ * (cantwellc/QEC_LDPC, paths relative to the repository root).
+ *
+ * Threading: a qec_code is immutable after creation and may be shared.  Calls on
+ * one qec_decoder are serialised by the caller (like one DecoderCPU per OpenMP
+ * thread, QEC_LDPC/DecoderCPU.h:431); distinct decoders may be driven from
+ * distinct host threads.
+ */
+#ifndef QEC_LDPC_H
+#define QEC_LDPC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define QEC_LDPC_ABI_VERSION 1
+
+/* status codes */
+enum {
+    QEC_OK = 0,
+    QEC_ERR_ARG = -1,          /* bad argument (null pointer, out-of-range size) */
+    QEC_ERR_IO = -2,           /* file missing/unreadable ("Unable to find code file", Quantum_LDPC_Code.h:78) */
+    QEC_ERR_FORMAT = -3,       /* malformed code file */
+    QEC_ERR_UNSUPPORTED = -4,  /* code shape the GPU engine does not handle */
+    QEC_ERR_HIP = -5,          /* HIP runtime error / no GPU */
+    QEC_ERR_NOMEM = -6
+};
+
+/* ErrorCode bit flags, identical to Decoder::ErrorCode (QEC_LDPC/Decoder.h:14-23) */
+enum {
+    QEC_SUCCESS = 0,
+    QEC_SYNDROME_FAIL_X = 1 << 0,
+    QEC_SYNDROME_FAIL_Z = 1 << 1,
+    QEC_SYNDROME_FAIL_XZ = QEC_SYNDROME_FAIL_X | QEC_SYNDROME_FAIL_Z,
+    QEC_CONVERGENCE_FAIL_X = 1 << 2,
+    QEC_CONVERGENCE_FAIL_Z = 1 << 3,
+    QEC_CONVERGENCE_FAIL_XZ = QEC_CONVERGENCE_FAIL_X | QEC_CONVERGENCE_FAIL_Z
+};
+
+/* BP stop rules */
+enum {
+    QEC_STOP_REF = 0,      /* DecoderCPU::BeliefPropogation (DecoderCPU.h:280-291): convergence test at n % 10 == 0 */
+    QEC_STOP_FIXED = 1,    /* exactly maxIterations iterations (the headline "fixed BP iters") */
+    QEC_STOP_SYNDROME = 2  /* stop once the hard decision satisfies the syndrome (per sector) */
+};
+
+enum { QEC_SECTOR_X = 0, QEC_SECTOR_Z = 1 };
+
+typedef struct qec_code qec_code;
+typedef struct qec_decoder qec_decoder;
+
+/* CodeStatistics (QEC_LDPC/CodeStatistics.h:5-20) counters */
+typedef struct {
+    uint32_t randSeed;
+    uint32_t numErrorsTested;
+    uint32_t numXErrorsTested;
+    uint32_t numZErrorsTested;
+    uint32_t errorWeight;
+    uint32_t corrected;
+    uint32_t syndromeErrorsX;
+    uint32_t syndromeErrorsZ;
+    uint32_t logicalErrors;
+    uint32_t convergenceFailX;
+    uint32_t convergenceFailZ;
+    int64_t durationMicroSeconds;
+} qec_stats;
+
+/* ---- diagnostics ---------------------------------------------------------- */
+const char* qec_last_error(void);  /* message of the last failing call on this thread */
+int qec_abi_version(void);         /* QEC_LDPC_ABI_VERSION */
+
+/* ---- code model ----------------------------------------------------------- */
+/* Replaces Quantum_LDPC_Code::createFromFile (QEC_LDPC/Quantum_LDPC_Code.h:26-80):
+ * 4-line text file "J K L P sigma tau" / HX / HZ / I-P.  NULL on error. */
+qec_code* qec_code_load(const char* path);
+/* Replaces the QC_LDPC_CSS(J,K,L,P,sigma,tau) generator (QEC_LDPC/QEC_LDPC_CSS.cu:5-131).
+ * Generated codes carry no I-P matrix (the reference never generates one). */
+qec_code* qec_code_generate(int J, int K, int L, int P, int sigma, int tau);
+int qec_code_free(qec_code* code);
+/* J K L P sigma tau n numEqsX numEqsZ (Quantum_LDPC_Code.h:10-20) into out[9] */
+int qec_code_params(const qec_code* code, int* out9);
+/* circulant shift of every P x P block, J x L (X) or K x L (Z), row-major;
+ * returns QEC_ERR_UNSUPPORTED if the code is not a circulant-permutation QC code */
+int qec_code_exponents(const qec_code* code, int sector, int* out);
+/* dense parity-check matrix pcmX / pcmZ (m x n, 0/1) */
+int qec_code_pcm(const qec_code* code, int sector, uint8_t* out);
+/* "[J=..,K=..,L=..,P=..,s=..,t=..][[n=..,k=..]]" (Quantum_LDPC_Code.h:145-150) */
+int qec_code_describe(const qec_code* code, char* buf, size_t len);
+/* Quantum_LDPC_Code::GetSyndromeX/Z (Quantum_LDPC_Code.h:94-124) for B error vectors,
+ * e: B x n (0/1) -> s: B x m (host memory) */
+int qec_code_syndrome(const qec_code* code, int sector, const uint8_t* e, size_t B, uint8_t* s);
+/* Quantum_LDPC_Code::CheckLogicalError (Quantum_LDPC_Code.h:126-142) on the
+ * residual [ex | ez] of B samples; out[b] = 1 if logical error */
+int qec_code_check_logical(const qec_code* code, const uint8_t* ex, const uint8_t* ez, size_t B, uint8_t* out);
+
+/* ---- decoder (DecoderGPU, QEC_LDPC/DecoderGPU.h:11-281) ------------------- */
+/* Replaces DecoderGPU(Quantum_LDPC_Code) (DecoderGPU.h:117-130).  device = HIP
+ * device ordinal (>= 0; there is no CPU engine in the product).  max_batch sizes
+ * the host-pointer staging buffers (grown on demand). */
+qec_decoder* qec_decoder_create(const qec_code* code, int device, size_t max_batch);
+int qec_decoder_destroy(qec_decoder* dec);
+/* which kernel variant serves this code: writes a short name (e.g. "wave-circulant P=61 G=1") */
+int qec_decoder_describe(const qec_decoder* dec, char* buf, size_t len);
+
+/* Batched Decoder::Decode (QEC_LDPC/Decoder.h:40-41, semantics of
+ * DecoderCPU::Decode, DecoderCPU.h:317-390) on HOST buffers; synchronous.
+ *   sX: B x numEqsX, sZ: B x numEqsZ   syndromes (0/1 bytes)
+ *   eX, eZ: B x n                      decoded error estimates (0/1 bytes)
+ *   flags: B                           ErrorCode bits per syndrome pair
+ *   iters: B x 2 (optional)            BP iterations executed (X, Z)
+ *   q_final: B x (numEqsX+numEqsZ) x L (optional) final variable->check messages,
+ *            [check][slot] with slots in ascending variable order (X block first)
+ * errorProbability / maxIterations as in Decode; stop = QEC_STOP_*. */
+int qec_decode_batch(qec_decoder* dec, const uint8_t* sX, const uint8_t* sZ, size_t B,
+                     float errorProbability, int maxIterations, int stop,
+                     uint8_t* eX, uint8_t* eZ, uint8_t* flags, int32_t* iters, float* q_final);
+/* Same on DEVICE buffers (same layouts), enqueued on `stream` (hipStream_t or NULL),
+ * asynchronous: no host synchronisation, no allocation (graph-capturable). */
+int qec_decode_batch_dev(qec_decoder* dec, const uint8_t* sX, const uint8_t* sZ, size_t B,
+                         float errorProbability, int maxIterations, int stop,
+                         uint8_t* eX, uint8_t* eZ, uint8_t* flags, int32_t* iters, float* q_final,
+                         void* stream);
+
+/* ---- Monte-Carlo caller side (DecoderCPU::GetStatistics, DecoderCPU.h:392-530) */
+/* The reference's fixed-weight sampler (DecoderCPU.h:448-459, RandomErrorGenerator.h:31-44):
+ * one mt19937(seed) stream, VS2015 uniform_int_distribution, W x (index, type) draws per
+ * sample.  x, z: count x n (0/1). */
+int qec_sample_fixed_weight(uint32_t seed, int W, size_t count, int n, uint8_t* x, uint8_t* z);
+/* Decoder::GetStatistics(errorWeight, numErrors, errorProbability, maxIterations, seed)
+ * (Decoder.h:44-47): samples numErrors errors exactly as the reference does, decodes them on
+ * the GPU (reference stop rule) and fills the CodeStatistics counters.  The reference tests
+ * (numErrors / nThreads) * nThreads samples; pass nThreads = 1 to test all numErrors. */
+int qec_get_statistics(qec_decoder* dec, int errorWeight, int numErrors, float errorProbability,
+                       int maxIterations, uint32_t seed, int nThreads, qec_stats* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* QEC_LDPC_H */

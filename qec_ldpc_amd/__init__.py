@@ -1,0 +1,300 @@
+"""qec_ldpc_amd -- Python view of libqecldpc.so, the MI355X belief-propagation
+decoder for quasi-cyclic CSS quantum LDPC codes.
+
+Mirrors the reference's interface (cantwellc/QEC_LDPC):
+  * Quantum_LDPC_Code.createFromFile / GetSyndromeX / GetSyndromeZ / CheckLogicalError
+    (QEC_LDPC/Quantum_LDPC_Code.h:26-142)
+  * QC_LDPC_CSS(J, K, L, P, sigma, tau) generator (QEC_LDPC/QEC_LDPC_CSS.cu:5-131)
+  * DecoderGPU(code).Decode / GetStatistics (QEC_LDPC/Decoder.h:40-47, DecoderGPU.h:117-280)
+plus the batched entry points the GPU engine is built around (decode_batch,
+decode_batch_dev).  Every call goes through the C ABI declared in
+include/qec_ldpc.h; there is no CPU decoding path in this package.  If the
+shared object is missing the import of the library fails loudly.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libqecldpc.so")
+
+SUCCESS = 0
+SYNDROME_FAIL_X = 1
+SYNDROME_FAIL_Z = 2
+CONVERGENCE_FAIL_X = 4
+CONVERGENCE_FAIL_Z = 8
+STOP = {"ref": 0, "fixed": 1, "syndrome": 2}
+
+# every symbol include/qec_ldpc.h declares
+EXPORTS = (
+    "qec_last_error", "qec_abi_version",
+    "qec_code_load", "qec_code_generate", "qec_code_free", "qec_code_params", "qec_code_exponents",
+    "qec_code_pcm", "qec_code_describe", "qec_code_syndrome", "qec_code_check_logical",
+    "qec_decoder_create", "qec_decoder_destroy", "qec_decoder_describe",
+    "qec_decode_batch", "qec_decode_batch_dev",
+    "qec_sample_fixed_weight", "qec_get_statistics",
+)
+
+
+class QecError(RuntimeError):
+    pass
+
+
+class Stats(ctypes.Structure):
+    """qec_stats == CodeStatistics counters (QEC_LDPC/CodeStatistics.h:5-20)."""
+    _fields_ = [("randSeed", ctypes.c_uint32), ("numErrorsTested", ctypes.c_uint32),
+                ("numXErrorsTested", ctypes.c_uint32), ("numZErrorsTested", ctypes.c_uint32),
+                ("errorWeight", ctypes.c_uint32), ("corrected", ctypes.c_uint32),
+                ("syndromeErrorsX", ctypes.c_uint32), ("syndromeErrorsZ", ctypes.c_uint32),
+                ("logicalErrors", ctypes.c_uint32), ("convergenceFailX", ctypes.c_uint32),
+                ("convergenceFailZ", ctypes.c_uint32), ("durationMicroSeconds", ctypes.c_int64)]
+
+    def as_dict(self):
+        return {k: int(getattr(self, k)) for k, _ in self._fields_}
+
+
+_lib = None
+
+
+def lib():
+    """The loaded libqecldpc.so (raises if it was not built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise QecError("libqecldpc.so not built (%s); run `make` or __graft_entry__.build()" % LIB_PATH)
+        L = ctypes.CDLL(LIB_PATH)
+        vp, i, f, sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_size_t
+        sig = {
+            "qec_last_error": (ctypes.c_char_p, []),
+            "qec_abi_version": (i, []),
+            "qec_code_load": (vp, [ctypes.c_char_p]),
+            "qec_code_generate": (vp, [i, i, i, i, i, i]),
+            "qec_code_free": (i, [vp]),
+            "qec_code_params": (i, [vp, vp]),
+            "qec_code_exponents": (i, [vp, i, vp]),
+            "qec_code_pcm": (i, [vp, i, vp]),
+            "qec_code_describe": (i, [vp, ctypes.c_char_p, sz]),
+            "qec_code_syndrome": (i, [vp, i, vp, sz, vp]),
+            "qec_code_check_logical": (i, [vp, vp, vp, sz, vp]),
+            "qec_decoder_create": (vp, [vp, i, sz]),
+            "qec_decoder_destroy": (i, [vp]),
+            "qec_decoder_describe": (i, [vp, ctypes.c_char_p, sz]),
+            "qec_decode_batch": (i, [vp, vp, vp, sz, f, i, i, vp, vp, vp, vp, vp]),
+            "qec_decode_batch_dev": (i, [vp, vp, vp, sz, f, i, i, vp, vp, vp, vp, vp, vp]),
+            "qec_sample_fixed_weight": (i, [ctypes.c_uint32, i, sz, i, vp, vp]),
+            "qec_get_statistics": (i, [vp, i, i, f, i, ctypes.c_uint32, i, ctypes.POINTER(Stats)]),
+        }
+        for name, (res, args) in sig.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def last_error():
+    return lib().qec_last_error().decode()
+
+
+def _check(rc, what):
+    if rc != 0:
+        raise QecError("%s failed (%d): %s" % (what, rc, last_error()))
+
+
+def _ptr(a):
+    if a is None:
+        return None
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def _u8(a, shape):
+    a = np.ascontiguousarray(a, dtype=np.uint8)
+    if a.shape != shape:
+        a = a.reshape(shape)
+    return a
+
+
+class Quantum_LDPC_Code:
+    """Code model (QEC_LDPC/Quantum_LDPC_Code.h:7-150)."""
+
+    def __init__(self, handle):
+        if not handle:
+            raise QecError(last_error())
+        self._h = ctypes.c_void_p(handle)
+        v = np.zeros(9, dtype=np.int32)
+        _check(lib().qec_code_params(self._h, _ptr(v)), "qec_code_params")
+        (self.J, self.K, self.L, self.P, self.sigma, self.tau, self.n, self.numEqsX,
+         self.numEqsZ) = (int(x) for x in v)
+
+    @staticmethod
+    def createFromFile(path):
+        h = lib().qec_code_load(os.fsencode(path))
+        if not h:
+            raise QecError(last_error())
+        return Quantum_LDPC_Code(h)
+
+    load = createFromFile
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h and _lib is not None:
+            _lib.qec_code_free(h)
+            self._h = None
+
+    @property
+    def handle(self):
+        return self._h
+
+    def describe(self):
+        buf = ctypes.create_string_buffer(256)
+        _check(lib().qec_code_describe(self._h, buf, 256), "qec_code_describe")
+        return buf.value.decode()
+
+    __str__ = describe
+
+    def exponents(self, sector):
+        R = self.K if sector else self.J
+        e = np.zeros((R, self.L), dtype=np.int32)
+        _check(lib().qec_code_exponents(self._h, int(sector), _ptr(e)), "qec_code_exponents")
+        return e
+
+    def pcm(self, sector):
+        m = self.numEqsZ if sector else self.numEqsX
+        h = np.zeros((m, self.n), dtype=np.uint8)
+        _check(lib().qec_code_pcm(self._h, int(sector), _ptr(h)), "qec_code_pcm")
+        return h
+
+    @property
+    def pcmX(self):
+        return self.pcm(0)
+
+    @property
+    def pcmZ(self):
+        return self.pcm(1)
+
+    def syndrome(self, sector, errors):
+        """Batched GetSyndromeX/Z: errors [B, n] -> [B, m]."""
+        e = np.atleast_2d(np.ascontiguousarray(errors, dtype=np.uint8))
+        m = self.numEqsZ if sector else self.numEqsX
+        s = np.empty((e.shape[0], m), dtype=np.uint8)
+        _check(lib().qec_code_syndrome(self._h, int(sector), _ptr(e), e.shape[0], _ptr(s)), "qec_code_syndrome")
+        return s
+
+    def GetSyndromeX(self, errors):
+        return self.syndrome(0, errors)[0]
+
+    def GetSyndromeZ(self, errors):
+        return self.syndrome(1, errors)[0]
+
+    def check_logical(self, ex, ez):
+        ex = np.atleast_2d(np.ascontiguousarray(ex, dtype=np.uint8))
+        ez = np.atleast_2d(np.ascontiguousarray(ez, dtype=np.uint8))
+        out = np.empty(ex.shape[0], dtype=np.uint8)
+        _check(lib().qec_code_check_logical(self._h, _ptr(ex), _ptr(ez), ex.shape[0], _ptr(out)),
+               "qec_code_check_logical")
+        return out.astype(bool)
+
+    def CheckLogicalError(self, errors):
+        errors = np.asarray(errors)
+        return bool(self.check_logical(errors[: self.n], errors[self.n:])[0])
+
+
+def QC_LDPC_CSS(J, K, L, P, sigma, tau):
+    """Generated code (QEC_LDPC/QEC_LDPC_CSS.cu:5-131); carries no I-P matrix."""
+    h = lib().qec_code_generate(J, K, L, P, sigma, tau)
+    if not h:
+        raise QecError(last_error())
+    return Quantum_LDPC_Code(h)
+
+
+def sample_fixed_weight(seed, W, count, n):
+    """The reference's fixed-weight sampler stream (DecoderCPU.h:448-459)."""
+    x = np.empty((count, n), dtype=np.uint8)
+    z = np.empty((count, n), dtype=np.uint8)
+    _check(lib().qec_sample_fixed_weight(seed & 0xFFFFFFFF, W, count, n, _ptr(x), _ptr(z)),
+           "qec_sample_fixed_weight")
+    return x, z
+
+
+class DecoderGPU:
+    """MI355X BP engine behind the reference's DecoderGPU slot (QEC_LDPC/DecoderGPU.h)."""
+
+    def __init__(self, code, device=0):
+        self.code = code
+        h = lib().qec_decoder_create(code.handle, int(device), 0)
+        if not h:
+            raise QecError(last_error())
+        self._h = ctypes.c_void_p(h)
+        self.device = device
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h and _lib is not None:
+            _lib.qec_decoder_destroy(h)
+            self._h = None
+
+    def describe(self):
+        buf = ctypes.create_string_buffer(256)
+        _check(lib().qec_decoder_describe(self._h, buf, 256), "qec_decoder_describe")
+        return buf.value.decode()
+
+    def decode_batch(self, sX, sZ, p, max_iter, stop="ref", want_iters=False, want_q=False):
+        """Host-buffer batch decode -> (eX, eZ, flags, iters|None, q|None)."""
+        c = self.code
+        sX = np.atleast_2d(sX)
+        B = sX.shape[0]
+        sX = _u8(sX, (B, c.numEqsX))
+        sZ = _u8(sZ, (B, c.numEqsZ))
+        eX = np.empty((B, c.n), dtype=np.uint8)
+        eZ = np.empty((B, c.n), dtype=np.uint8)
+        flags = np.empty(B, dtype=np.uint8)
+        iters = np.empty((B, 2), dtype=np.int32) if want_iters else None
+        q = np.empty((B, (c.numEqsX + c.numEqsZ) * c.L), dtype=np.float32) if want_q else None
+        _check(lib().qec_decode_batch(self._h, _ptr(sX), _ptr(sZ), B, float(p), int(max_iter), STOP[stop],
+                                      _ptr(eX), _ptr(eZ), _ptr(flags), _ptr(iters), _ptr(q)), "qec_decode_batch")
+        return eX, eZ, flags, iters, q
+
+    def decode_batch_dev(self, sX, sZ, p, max_iter, stop, eX, eZ, flags, iters=None, q=None, stream=None):
+        """Device-buffer batch decode on torch tensors (or raw int pointers), async on `stream`
+        (a torch.cuda.Stream, a raw hipStream_t int, or None = torch's current stream)."""
+        def addr(t):
+            if t is None:
+                return None
+            return t if isinstance(t, int) else t.data_ptr()
+        B = sX.shape[0] if hasattr(sX, "shape") else None
+        if B is None:
+            raise QecError("decode_batch_dev needs tensors with a shape")
+        if stream is None:
+            import torch
+            stream = torch.cuda.current_stream().cuda_stream
+        elif not isinstance(stream, int):
+            stream = stream.cuda_stream
+        _check(lib().qec_decode_batch_dev(self._h, addr(sX), addr(sZ), B, float(p), int(max_iter), STOP[stop],
+                                          addr(eX), addr(eZ), addr(flags), addr(iters), addr(q),
+                                          ctypes.c_void_p(stream)), "qec_decode_batch_dev")
+
+    def Decode(self, syndromeX, syndromeZ, errorProbability, maxIterations):
+        """Decoder::Decode for one syndrome pair -> (ErrorCode, outErrorsX, outErrorsZ)."""
+        eX, eZ, flags, _, _ = self.decode_batch(np.asarray(syndromeX)[None], np.asarray(syndromeZ)[None],
+                                                errorProbability, maxIterations, "ref")
+        return int(flags[0]), eX[0].astype(np.int32), eZ[0].astype(np.int32)
+
+    def GetStatistics(self, errorWeight, numErrors, errorProbability, maxIterations, seed=None, nThreads=1):
+        if seed is None:
+            seed = int.from_bytes(os.urandom(4), "little")
+        st = Stats()
+        _check(lib().qec_get_statistics(self._h, errorWeight, numErrors, float(errorProbability), maxIterations,
+                                        seed & 0xFFFFFFFF, nThreads, ctypes.byref(st)), "qec_get_statistics")
+        return st.as_dict()
+
+
+def format_statistics(code, st):
+    """CodeStatistics operator<< text block (QEC_LDPC/CodeStatistics.h:22-37)."""
+    return ("Code: %s\nRand Seed: %d\nDuration(micro-s): %d\nErrors Tested: %d\nErrors With X: %d\n"
+            "Errors With Z: %d\nError Weight: %d\nCorrected: %d\nSyndrome Errors X: %d\n"
+            "Syndrome Errors Z: %d\nLogical Errors: %d\nConvergence Fail X: %d\nConvergence Fail Z: %d\n"
+            % (code.describe(), st["randSeed"], st["durationMicroSeconds"], st["numErrorsTested"],
+               st["numXErrorsTested"], st["numZErrorsTested"], st["errorWeight"], st["corrected"],
+               st["syndromeErrorsX"], st["syndromeErrorsZ"], st["logicalErrors"], st["convergenceFailX"],
+               st["convergenceFailZ"]))

@@ -1,0 +1,53 @@
+// Internal declarations shared by the libqecldpc translation units.
+// Not part of the public interface (that is include/qec_ldpc.h).
+#pragma once
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../../include/qec_ldpc.h"
+
+namespace qec {
+
+// Thread-local last-error text behind qec_last_error().
+void set_error(const std::string& msg);
+int fail(int status, const std::string& msg);
+
+// Quantum_LDPC_Code (QEC_LDPC/Quantum_LDPC_Code.h:7-150) in circulant form.
+// The dense pcmX/pcmZ/iMinusP of the reference are kept for API parity; the
+// decoder itself only needs the exponent tables (one shift per P x P block).
+struct Code {
+    int J = 0, K = 0, L = 0, P = 0, sigma = 0, tau = 0;
+    int n = 0, mX = 0, mZ = 0;
+    std::vector<uint8_t> pcmX, pcmZ;   // m x n dense, as read / generated
+    std::vector<uint8_t> imp;          // 2n x 2n dense I-P (empty for generated codes)
+    bool is_qc = false;                // every block a circulant permutation matrix
+    std::vector<int> EX, EZ;           // J x L / K x L shifts in [0, P): row i -> col (E + i) mod P
+    // Bit-packed I-P rows that are not all-zero (for CheckLogicalError).
+    int imp_words = 0;                 // u64 words per packed 2n-bit row
+    std::vector<uint64_t> imp_rows;    // nnz_rows x imp_words
+    std::string describe() const;      // operator<< of Quantum_LDPC_Code.h:145-150
+};
+
+int load_code(const char* path, Code& out);
+int generate_code(int J, int K, int L, int P, int sigma, int tau, Code& out);
+// Generator exponent tables (QEC_LDPC/QEC_LDPC_CSS.cu:37-90); returns false if sigma has no inverse.
+bool generator_exponents(int J, int K, int L, int P, int sigma, int tau, std::vector<int>& EX, std::vector<int>& EZ);
+void finalize_code(Code& c);  // derive circulant tables + packed I-P from the dense matrices
+
+// Host syndrome s = H e mod 2 via the circulant tables (or dense if not QC).
+void host_syndrome(const Code& c, int sector, const uint8_t* e, uint8_t* s);
+// CheckLogicalError (Quantum_LDPC_Code.h:126-142) on [ex | ez].
+bool host_check_logical(const Code& c, const uint8_t* ex, const uint8_t* ez);
+
+// std::mt19937 + VS2015 uniform_int_distribution, the
+// stream the reference's published seeds were drawn from.
+struct Mt19937 {
+    uint32_t mt[624];
+    int idx;
+    explicit Mt19937(uint32_t seed);
+    uint32_t next();
+    uint32_t msvc_uniform(uint32_t N);  // uniform_int_distribution<int>(0, N-1)
+};
+
+}  // namespace qec

@@ -1,0 +1,78 @@
+"""BASELINE.json configs at full size on the GPU (configs[1]: P7 x 65536 @ 20 fixed
+iterations, configs[2]: P61 x 65536 @ 50 fixed iterations), checked through
+size-independent properties: oracle parity on a random subsample, determinism,
+batch-split invariance, device-pointer == host-pointer entry point, and the
+decision syndrome identity (flags say SYNDROME_FAIL exactly when H e != s)."""
+import numpy as np
+import pytest
+
+import qec_ldpc_amd as q
+from oracle.oracle import OracleCode
+from qec_ldpc_amd.synthetic import depolarizing_errors
+
+pytestmark = pytest.mark.gpu
+
+CONFIGS = [("P7", 65536, 20, 0.02), ("P61", 65536, 50, 0.01)]
+
+
+@pytest.fixture(scope="module", params=CONFIGS, ids=[c[0] for c in CONFIGS])
+def run(request, code_paths):
+    key, B, N, p = request.param
+    code = q.Quantum_LDPC_Code.createFromFile(code_paths[key])
+    dec = q.DecoderGPU(code, 0)
+    x, z = depolarizing_errors(code.n, 0, B, p)
+    sX, sZ = code.syndrome(0, x), code.syndrome(1, z)
+    out = dec.decode_batch(sX, sZ, p, N, "fixed", want_iters=True)
+    return dict(key=key, code=code, dec=dec, B=B, N=N, p=p, sX=sX, sZ=sZ, x=x, z=z, out=out,
+                path=code_paths[key])
+
+
+def test_oracle_subsample(run):
+    rng = np.random.default_rng(123)
+    idx = np.sort(rng.choice(run["B"], 256, replace=False))
+    o = OracleCode(run["path"]).decode_batch(run["sX"][idx], run["sZ"][idx], run["p"], run["N"], "fixed")
+    for a, b in zip(run["out"][:4], o[:4]):
+        assert np.array_equal(a[idx], b)
+
+
+def test_deterministic(run):
+    again = run["dec"].decode_batch(run["sX"], run["sZ"], run["p"], run["N"], "fixed", want_iters=True)
+    for a, b in zip(run["out"][:4], again[:4]):
+        assert np.array_equal(a, b)
+
+
+def test_split_invariance(run):
+    h = run["B"] // 2 + 5
+    lo = run["dec"].decode_batch(run["sX"][:h], run["sZ"][:h], run["p"], run["N"], "fixed")
+    hi = run["dec"].decode_batch(run["sX"][h:], run["sZ"][h:], run["p"], run["N"], "fixed")
+    for k in range(3):
+        assert np.array_equal(np.concatenate([lo[k], hi[k]]), run["out"][k])
+
+
+def test_device_entry_point(run):
+    import torch
+    dev = torch.device("cuda:0")
+    c = run["code"]
+    B = run["B"]
+    sX = torch.from_numpy(run["sX"]).to(dev)
+    sZ = torch.from_numpy(run["sZ"]).to(dev)
+    eX = torch.empty((B, c.n), dtype=torch.uint8, device=dev)
+    eZ = torch.empty((B, c.n), dtype=torch.uint8, device=dev)
+    fl = torch.empty(B, dtype=torch.uint8, device=dev)
+    it = torch.empty((B, 2), dtype=torch.int32, device=dev)
+    run["dec"].decode_batch_dev(sX, sZ, run["p"], run["N"], "fixed", eX, eZ, fl, it)
+    torch.cuda.synchronize()
+    for a, b in zip((eX, eZ, fl, it), run["out"][:4]):
+        assert np.array_equal(a.cpu().numpy(), b)
+
+
+def test_flags_consistent_with_syndromes(run):
+    c = run["code"]
+    eX, eZ, flags, iters, _ = run["out"]
+    synx = (c.syndrome(0, eX) != run["sX"]).any(1)
+    synz = (c.syndrome(1, eZ) != run["sZ"]).any(1)
+    assert np.array_equal(synx, (flags & q.SYNDROME_FAIL_X) != 0)
+    assert np.array_equal(synz, (flags & q.SYNDROME_FAIL_Z) != 0)
+    assert (iters == run["N"]).all()
+    # the decoder actually decodes: most low-p samples satisfy their syndromes
+    assert synx.mean() < 0.5 and synz.mean() < 0.5

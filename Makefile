@@ -3,7 +3,7 @@
 HIPCC    ?= /opt/rocm/bin/hipcc
 ARCH     ?= gfx950
 # IEEE fp32 exactly as written: no contraction, no fast-math, denormals preserved.
-HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -Wall -Wno-unused-function
+HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -fno-slp-vectorize -Wall -Wno-unused-function
 CSRC     := qec_ldpc_amd/csrc
 OBJ      := build/obj
 LIB      := qec_ldpc_amd/libqecldpc.so

@@ -40,7 +40,19 @@
 
 namespace qec {
 
+// Compile-time design options (tools/kbench sweeps them; the defaults are the measured best):
+//   QEC_RELABEL      spanning-tree lane relabelling (fewer ds_bpermute, but more distinct shifts)
+//   QEC_MASK_SELECT  rotation base chosen by a constant lane mask instead of hoisted addresses
+#ifndef QEC_RELABEL
+#define QEC_RELABEL 0
+#endif
+#ifndef QEC_MASK_SELECT
+#define QEC_MASK_SELECT 0
+#endif
+
 constexpr int kMaxRL = 128;  // largest R*L a kernel argument block carries
+constexpr int kMaxR = 16;
+constexpr int kMaxL = 32;
 
 struct BpArgs {
     const uint8_t* sX;
@@ -54,9 +66,32 @@ struct BpArgs {
     int P, G, n, mX, mZ;
     float errorProbability;
     int maxIter, stop;
-    int EX[kMaxRL];
-    int EZ[kMaxRL];
+    // lane-relabelled circulant tables (see relabel() below)
+    int SX[kMaxRL], SZ[kMaxRL];  // rotation of block (r, l) between check and variable views
+    int DX[kMaxR], DZ[kMaxR];    // check-view lane lambda holds check (r, (lambda + D[r]) mod P)
+    int CX[kMaxL], CZ[kMaxL];    // var-view lane mu holds variable (l, (mu + C[l]) mod P)
 };
+
+// ---- lane relabelling ------------------------------------------------------
+// Block (r, l) of a sector is the circulant "check (r, i) <-> variable (l, (E[r][l] + i) mod P)".
+// Storing check (r, i) in lane (i - D[r]) mod P and variable (l, j) in lane (j - C[l]) mod P
+// turns the block's check->variable lane rotation into S[r][l] = (E[r][l] + D[r] - C[l]) mod P.
+// With C[l] = E[0][l] and D[r] = (C[0] - E[r][0]) mod P the R + L - 1 blocks of row 0 and
+// column 0 need no rotation at all (a spanning tree of the block graph), so those edges skip
+// the ds_bpermute in both directions.  Arithmetic (and so every output bit) is unchanged.
+inline void relabel(const int* E, int R, int L, int P, int* S, int* D, int* C)
+{
+    if (!QEC_RELABEL) {
+        for (int k = 0; k < R * L; ++k) S[k] = E[k];
+        for (int r = 0; r < R; ++r) D[r] = 0;
+        for (int l = 0; l < L; ++l) C[l] = 0;
+        return;
+    }
+    for (int l = 0; l < L; ++l) C[l] = E[l];
+    for (int r = 0; r < R; ++r) D[r] = ((C[0] - E[r * L]) % P + P) % P;
+    for (int r = 0; r < R; ++r)
+        for (int l = 0; l < L; ++l) S[r * L + l] = ((E[r * L + l] + D[r] - C[l]) % P + P) % P;
+}
 
 // ---- shift providers -------------------------------------------------------
 // Runtime: exponents read from the kernel-argument block.  table() launders the
@@ -65,16 +100,21 @@ struct BpArgs {
 // live registers.
 struct RuntimeShifts {
     static constexpr bool kStatic = false;
+    static constexpr int kP = 0;
     __device__ static int P(const BpArgs& a) { return a.P; }
     template <int SEC>
     __device__ static const int* table(const BpArgs& a)
     {
-        const int* t = SEC ? a.EZ : a.EX;
+        const int* t = SEC ? a.SZ : a.SX;
         asm volatile("" : "+s"(t));
         return t;
     }
     template <int SEC, int L>
     __device__ static int shift(const int* t, int r, int l) { return t[r * L + l]; }
+    template <int SEC>
+    __device__ static int rowoff(const BpArgs& a, int r) { return SEC ? a.DZ[r] : a.DX[r]; }
+    template <int SEC>
+    __device__ static int coloff(const BpArgs& a, int l) { return SEC ? a.CZ[l] : a.CX[l]; }
 };
 
 // Compile-time: exponent tables produced by the QC_LDPC_CSS generator formula
@@ -83,9 +123,13 @@ struct RuntimeShifts {
 template <int J_, int K_, int L_, int P_, int S_, int T_>
 struct GeneratedShifts {
     static constexpr bool kStatic = true;
+    static constexpr int kP = P_;
     struct Tables {
         int EX[J_][L_];
         int EZ[K_][L_];
+        int SX[J_][L_], SZ[K_][L_];
+        int DX[J_], DZ[K_];
+        int CX[L_], CZ[L_];
     };
     static constexpr long pw(long base, long e)
     {
@@ -106,6 +150,14 @@ struct GeneratedShifts {
         for (int k = 0; k < K_; ++k)
             for (int l = 0; l < L_; ++l)
                 t.EZ[k][l] = (int)(((((l < L_ / 2) ? (T_ * sp(l - k - 1)) % P_ : P_ - sp(k + l)) % P_) + P_) % P_);
+        // relabel() on the 2-D tables (same rule, written out for constant evaluation)
+        for (int l = 0; l < L_; ++l) { t.CX[l] = QEC_RELABEL ? t.EX[0][l] : 0; t.CZ[l] = QEC_RELABEL ? t.EZ[0][l] : 0; }
+        for (int r = 0; r < J_; ++r) t.DX[r] = QEC_RELABEL ? ((t.CX[0] - t.EX[r][0]) % P_ + P_) % P_ : 0;
+        for (int r = 0; r < K_; ++r) t.DZ[r] = QEC_RELABEL ? ((t.CZ[0] - t.EZ[r][0]) % P_ + P_) % P_ : 0;
+        for (int r = 0; r < J_; ++r)
+            for (int l = 0; l < L_; ++l) t.SX[r][l] = ((t.EX[r][l] + t.DX[r] - t.CX[l]) % P_ + P_) % P_;
+        for (int r = 0; r < K_; ++r)
+            for (int l = 0; l < L_; ++l) t.SZ[r][l] = ((t.EZ[r][l] + t.DZ[r] - t.CZ[l]) % P_ + P_) % P_;
         return t;
     }
     static constexpr Tables tabs = make();
@@ -113,7 +165,11 @@ struct GeneratedShifts {
     template <int SEC>
     __device__ static const int* table(const BpArgs&) { return nullptr; }
     template <int SEC, int L>
-    __device__ static constexpr int shift(const int*, int r, int l) { return SEC ? tabs.EZ[r][l] : tabs.EX[r][l]; }
+    __device__ static constexpr int shift(const int*, int r, int l) { return SEC ? tabs.SZ[r][l] : tabs.SX[r][l]; }
+    template <int SEC>
+    __device__ static constexpr int rowoff(const BpArgs&, int r) { return SEC ? tabs.DZ[r] : tabs.DX[r]; }
+    template <int SEC>
+    __device__ static constexpr int coloff(const BpArgs&, int l) { return SEC ? tabs.CZ[l] : tabs.CX[l]; }
 };
 
 // ---- lane helpers ----------------------------------------------------------
@@ -123,13 +179,57 @@ __device__ __forceinline__ float bperm(int addr, float v)
 }
 __device__ __forceinline__ int bperm_i(int addr, int v) { return __builtin_amdgcn_ds_bpermute(addr, v); }
 
-// byte address for ds_bpermute: lane (gb + (i - s) mod P), s in [0, P)
-__device__ __forceinline__ int rot_addr(int i, int gb, int s, int P)
+// Rotation inside a lane group: the value of lane gb + (i - s) mod P, s in [0, P).
+// ds_bpermute selects lane ((addr + offset) >> 2) & 63, so with the two per-lane bases
+//   b0 = 4 (gb + i)  and  b1 = b0 + 4P
+// the address is (i < s ? b1 : b0) + (256 - 4 s): the constant folds into the
+// instruction's offset field and only the base choice costs a VALU op.  For the
+// generated (compile-time) tables "i < s" is a constant lane mask held in an SGPR
+// pair, so the choice is a single v_cndmask; the runtime tables compare instead.
+// s == 0 is the identity and emits nothing.
+struct Lane {
+    int i, gb;   // in-group index, group base lane
+    int b0, b1;  // bpermute bases (laundered once per iteration so they stay cheap to reuse)
+};
+
+template <int P_>
+__device__ constexpr unsigned long long lanes_below(int s)
 {
-    int t = i - s;
-    t += (t < 0) ? P : 0;
-    return (gb + t) << 2;
+    unsigned long long m = 0;
+    for (int g = 0; g < 64 / P_; ++g)
+        for (int k = 0; k < s; ++k) m |= 1ull << (g * P_ + k);
+    return m;
 }
+
+__device__ __forceinline__ int select_lanes(int a, int b, unsigned long long m)
+{
+    int r;
+    asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(m));
+    return r;
+}
+
+template <class SH>
+__device__ __forceinline__ int rot_addr(const Lane& ln, int s)
+{
+    int base;
+    if constexpr (SH::kStatic && QEC_MASK_SELECT)
+        base = select_lanes(ln.b0, ln.b1, lanes_below<SH::kP>(s));
+    else
+        base = (ln.i < s) ? ln.b1 : ln.b0;  // loop-invariant per s: hoisted by the compiler
+    return base + (256 - 4 * s);
+}
+
+template <class SH>
+__device__ __forceinline__ float rot(float v, const Lane& ln, int s)
+{
+    return s == 0 ? v : bperm(rot_addr<SH>(ln, s), v);
+}
+template <class SH>
+__device__ __forceinline__ int rot_i(int v, const Lane& ln, int s)
+{
+    return s == 0 ? v : bperm_i(rot_addr<SH>(ln, s), v);
+}
+__device__ __forceinline__ int wrap(int x, int P) { return x >= P ? x - P : x; }
 
 // true iff pred holds on every lane of this lane's group [gb, gb+P)
 __device__ __forceinline__ bool group_all(bool pred, int gb, int P)
@@ -180,7 +280,7 @@ __device__ __forceinline__ void check_pass(float (&msg)[R][L], uint32_t sbits)
 // LAST: the final iteration includes the self message (DecoderCPU.h:216).
 // Returns the hard-decision mask (bit l) of the new messages when HD is set.
 template <int R, int L, int SEC, bool LAST, bool HD, class SH>
-__device__ __forceinline__ uint32_t var_pass(const BpArgs& a, float (&msg)[R][L], int i, int gb, float pp,
+__device__ __forceinline__ uint32_t var_pass(const BpArgs& a, float (&msg)[R][L], const Lane& ln, float pp,
                                              float one_minus_pp)
 {
     const int P = SH::P(a);
@@ -192,7 +292,7 @@ __device__ __forceinline__ uint32_t var_pass(const BpArgs& a, float (&msg)[R][L]
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             const int sh = SH::template shift<SEC, L>(et, r, l);
-            gv[r] = bperm(rot_addr(i, gb, sh, P), msg[r][l]);
+            gv[r] = rot<SH>(msg[r][l], ln, sh);
             bv[r] = 1.0f - gv[r];
         }
         if constexpr (LAST) {
@@ -222,7 +322,7 @@ __device__ __forceinline__ uint32_t var_pass(const BpArgs& a, float (&msg)[R][L]
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             const int sh = SH::template shift<SEC, L>(et, r, l);
-            msg[r][l] = bperm(rot_addr(i, gb, sh == 0 ? 0 : P - sh, P), qv[r]);
+            msg[r][l] = rot<SH>(qv[r], ln, sh == 0 ? 0 : P - sh);
         }
     }
     return hdmask;
@@ -243,7 +343,7 @@ __device__ __forceinline__ bool lane_converged(const float (&msg)[R][L])
 // Syndrome of the hard decision (var view, bit l of hdmask) equals the input syndrome
 // on this lane's checks (r, i): GetSyndromeX/Z of Decode (DecoderCPU.h:380-384).
 template <int R, int L, int SEC, class SH>
-__device__ __forceinline__ bool lane_syndrome_ok(const BpArgs& a, uint32_t hdmask, uint32_t sbits, int i, int gb)
+__device__ __forceinline__ bool lane_syndrome_ok(const BpArgs& a, uint32_t hdmask, uint32_t sbits, const Lane& ln)
 {
     const int P = SH::P(a);
     const int* et = SH::template table<SEC>(a);
@@ -254,7 +354,7 @@ __device__ __forceinline__ bool lane_syndrome_ok(const BpArgs& a, uint32_t hdmas
 #pragma unroll
         for (int l = 0; l < L; ++l) {
             const int sh = SH::template shift<SEC, L>(et, r, l);
-            x ^= ((uint32_t)bperm_i(rot_addr(i, gb, sh == 0 ? 0 : P - sh, P), (int)hdmask) >> l) & 1u;
+            x ^= ((uint32_t)rot_i<SH>((int)hdmask, ln, sh == 0 ? 0 : P - sh) >> l) & 1u;
         }
         match &= (x == ((sbits >> r) & 1u));
     }
@@ -263,24 +363,28 @@ __device__ __forceinline__ bool lane_syndrome_ok(const BpArgs& a, uint32_t hdmas
 
 // One BP iteration; returns true if this group stops after it.
 template <int R, int L, int SEC, int STOP, bool LAST, class SH>
-__device__ __forceinline__ bool iteration(const BpArgs& a, float (&msg)[R][L], uint32_t sbits, int n, int i, int gb,
+__device__ __forceinline__ bool iteration(const BpArgs& a, float (&msg)[R][L], uint32_t sbits, int n, Lane& ln,
                                           float pp, float one_minus_pp)
 {
     const int P = SH::P(a);
+    // launder the permute bases so their per-rotation selects are recomputed inside the
+    // loop instead of being hoisted into ~2 R L live registers
+    if constexpr (QEC_MASK_SELECT) asm volatile("" : "+v"(ln.b0), "+v"(ln.b1));
     check_pass<R, L>(msg, sbits);
-    const uint32_t hdmask = var_pass<R, L, SEC, LAST, STOP == QEC_STOP_SYNDROME, SH>(a, msg, i, gb, pp, one_minus_pp);
+    const uint32_t hdmask = var_pass<R, L, SEC, LAST, STOP == QEC_STOP_SYNDROME, SH>(a, msg, ln, pp, one_minus_pp);
     if constexpr (STOP == QEC_STOP_REF) {
-        if (n % 10 == 0) return group_all(lane_converged<R, L>(msg), gb, P);  // DecoderCPU.h:287-290
+        if (n % 10 == 0) return group_all(lane_converged<R, L>(msg), ln.gb, P);  // DecoderCPU.h:287-290
     } else if constexpr (STOP == QEC_STOP_SYNDROME) {
-        return group_all(lane_syndrome_ok<R, L, SEC, SH>(a, hdmask, sbits, i, gb), gb, P);
+        return group_all(lane_syndrome_ok<R, L, SEC, SH>(a, hdmask, sbits, ln), ln.gb, P);
     }
     return false;
 }
 
 template <int R, int L, int SEC, int STOP, class SH>
-__device__ __forceinline__ void decode_sector(const BpArgs& a, int i, int gb, long long b, bool in_range, float pp,
+__device__ __forceinline__ void decode_sector(const BpArgs& a, Lane& ln, long long b, bool in_range, float pp,
                                               uint32_t& flags, int& iters_out)
 {
+    const int i = ln.i, gb = ln.gb;
     const int P = SH::P(a);
     const int m = R * P;
     const uint8_t* __restrict__ s = SEC ? a.sZ : a.sX;
@@ -289,7 +393,8 @@ __device__ __forceinline__ void decode_sector(const BpArgs& a, int i, int gb, lo
     uint32_t sbits = 0;
     if (in_range) {
 #pragma unroll
-        for (int r = 0; r < R; ++r) sbits |= (uint32_t)(s[b * m + r * P + i] & 1) << r;
+        for (int r = 0; r < R; ++r)
+            sbits |= (uint32_t)(s[b * m + r * P + wrap(i + SH::template rowoff<SEC>(a, r), P)] & 1) << r;
     }
 
     // InitVarNodes: every edge starts at p' (DecoderCPU.h:135-148, 265-267)
@@ -311,12 +416,12 @@ __device__ __forceinline__ void decode_sector(const BpArgs& a, int i, int gb, lo
         }
         if (active) {
             ++it;
-            if (iteration<R, L, SEC, STOP, false, SH>(a, msg, sbits, n, i, gb, pp, one_minus_pp)) active = false;
+            if (iteration<R, L, SEC, STOP, false, SH>(a, msg, sbits, n, ln, pp, one_minus_pp)) active = false;
         }
     }
     if (n == N - 1 && active) {
         ++it;
-        iteration<R, L, SEC, STOP, true, SH>(a, msg, sbits, n, i, gb, pp, one_minus_pp);
+        iteration<R, L, SEC, STOP, true, SH>(a, msg, sbits, n, ln, pp, one_minus_pp);
     }
 
     // ---- post-processing of Decode (DecoderCPU.h:354-384) ----
@@ -330,12 +435,12 @@ __device__ __forceinline__ void decode_sector(const BpArgs& a, int i, int gb, lo
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             const int sh = SH::template shift<SEC, L>(et, r, l);
-            hd |= bperm(rot_addr(i, gb, sh, P), msg[r][l]) >= 0.5f;
+            hd |= rot<SH>(msg[r][l], ln, sh) >= 0.5f;
         }
         hdmask |= (uint32_t)hd << l;
-        if (in_range) e[b * (long long)a.n + l * P + i] = (uint8_t)hd;
+        if (in_range) e[b * (long long)a.n + l * P + wrap(i + SH::template coloff<SEC>(a, l), P)] = (uint8_t)hd;
     }
-    const bool syn_ok = group_all(lane_syndrome_ok<R, L, SEC, SH>(a, hdmask, sbits, i, gb), gb, P);
+    const bool syn_ok = group_all(lane_syndrome_ok<R, L, SEC, SH>(a, hdmask, sbits, ln), gb, P);
 
     if (!syn_ok) flags |= SEC ? QEC_SYNDROME_FAIL_Z : QEC_SYNDROME_FAIL_X;
     if (!conv) flags |= SEC ? QEC_CONVERGENCE_FAIL_Z : QEC_CONVERGENCE_FAIL_X;
@@ -346,12 +451,24 @@ __device__ __forceinline__ void decode_sector(const BpArgs& a, int i, int gb, lo
 #pragma unroll
         for (int r = 0; r < R; ++r)
 #pragma unroll
-            for (int l = 0; l < L; ++l) a.q[qb + (long long)(r * P + i) * L + l] = msg[r][l];
+            for (int l = 0; l < L; ++l)
+                a.q[qb + (long long)(r * P + wrap(i + SH::template rowoff<SEC>(a, r), P)) * L + l] = msg[r][l];
     }
 }
 
-template <int RX, int RZ, int L, int STOP, class SH>
-__global__ __launch_bounds__(256) void bp_decode_kernel(const BpArgs a)
+// Tuning knobs (compile-time; tools/kbench/ sweeps them).
+#ifndef QEC_WAVES_PER_BLOCK
+#define QEC_WAVES_PER_BLOCK 4
+#endif
+#ifndef QEC_MIN_WAVES_PER_EU
+#define QEC_MIN_WAVES_PER_EU 0  // 0: per-variant defaults below
+#endif
+
+// MINW: minimum waves per SIMD the register allocator must allow (5 -> <= 96 VGPRs), measured
+// per variant with tools/kbench (P61: 5 waves beat 4 by 4 %; see profiles/).
+template <int RX, int RZ, int L, int STOP, class SH, int MINW>
+__global__ __launch_bounds__(64 * QEC_WAVES_PER_BLOCK, (QEC_MIN_WAVES_PER_EU ? QEC_MIN_WAVES_PER_EU : MINW))
+void bp_decode_kernel(const BpArgs a)
 {
     const int lane = threadIdx.x & 63;
     const long long wave = (long long)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
@@ -368,8 +485,9 @@ __global__ __launch_bounds__(256) void bp_decode_kernel(const BpArgs a)
     const float pp = 2.0f / 3.0f * a.errorProbability;
     uint32_t flags = 0;
     int itX = 0, itZ = 0;
-    decode_sector<RX, L, 0, STOP, SH>(a, i, gb, b, in_range, pp, flags, itX);
-    decode_sector<RZ, L, 1, STOP, SH>(a, i, gb, b, in_range, pp, flags, itZ);
+    Lane ln{i, gb, 4 * (gb + i), 4 * (gb + i + P)};
+    decode_sector<RX, L, 0, STOP, SH>(a, ln, b, in_range, pp, flags, itX);
+    decode_sector<RZ, L, 1, STOP, SH>(a, ln, b, in_range, pp, flags, itZ);
     if (in_range && i == 0) {
         a.flags[b] = (uint8_t)flags;
         if (a.iters != nullptr) {
@@ -389,38 +507,40 @@ struct Variant {
     const char* name;
 };
 
-template <int J, int K, int L, class SH>
+template <int J, int K, int L, class SH, int MINW>
 static Variant make_variant(int P, int S, int T, const char* name)
 {
     return Variant{J, K, L, P, S, T,
-                   {bp_decode_kernel<J, K, L, QEC_STOP_REF, SH>, bp_decode_kernel<J, K, L, QEC_STOP_FIXED, SH>,
-                    bp_decode_kernel<J, K, L, QEC_STOP_SYNDROME, SH>},
+                   {bp_decode_kernel<J, K, L, QEC_STOP_REF, SH, MINW>, bp_decode_kernel<J, K, L, QEC_STOP_FIXED, SH, MINW>,
+                    bp_decode_kernel<J, K, L, QEC_STOP_SYNDROME, SH, MINW>},
                    name};
 }
-template <int J, int K, int L>
+template <int J, int K, int L, int MINW = 1>
 static Variant rt()
 {
-    return make_variant<J, K, L, RuntimeShifts>(0, 0, 0, "wave-circulant runtime-shift");
+    return make_variant<J, K, L, RuntimeShifts, MINW>(0, 0, 0, "wave-circulant runtime-shift");
 }
-template <int J, int K, int L, int P, int S, int T>
+template <int J, int K, int L, int P, int S, int T, int MINW>
 static Variant gen()
 {
-    return make_variant<J, K, L, GeneratedShifts<J, K, L, P, S, T>>(P, S, T, "wave-circulant generated-shift");
+    return make_variant<J, K, L, GeneratedShifts<J, K, L, P, S, T>, MINW>(P, S, T, "wave-circulant generated-shift");
 }
 
 static const Variant kVariants[] = {
     // specialised: the two code files the reference ships
-    gen<4, 5, 10, 61, 9, 49>(),
-    gen<3, 3, 6, 7, 2, 3>(),
+    gen<4, 5, 10, 61, 9, 49, 5>(),
+    gen<3, 3, 6, 7, 2, 3, 8>(),
+#ifndef QEC_KBENCH_MINIMAL  // experiment builds (tools/kbench) only compile the shipped-code kernels
     // runtime shifts, any P <= 64 with these block shapes
     rt<4, 5, 10>(),
-    rt<3, 3, 6>(),
-    rt<2, 3, 6>(),
+    rt<3, 3, 6, 6>(),
+    rt<2, 3, 6, 6>(),
     rt<3, 4, 8>(),
     rt<4, 4, 8>(),
     rt<3, 5, 10>(),
     rt<4, 6, 12>(),
-    rt<2, 2, 4>(),
+    rt<2, 2, 4, 8>(),
+#endif
 };
 
 struct DecodeLaunch {
@@ -430,7 +550,7 @@ struct DecodeLaunch {
 const void* select_variant(const Code& c, std::string& name)
 {
     if (!c.is_qc || c.P > 64 || c.P < 1) return nullptr;
-    if (c.J * c.L > kMaxRL || c.K * c.L > kMaxRL) return nullptr;
+    if (c.J * c.L > kMaxRL || c.K * c.L > kMaxRL || c.J > kMaxR || c.K > kMaxR || c.L > kMaxL) return nullptr;
     for (const Variant& v : kVariants) {
         if (v.J != c.J || v.K != c.K || v.L != c.L) continue;
         if (v.P > 0) {
@@ -462,9 +582,9 @@ int launch_decode(const void* variant, const Code& c, const uint8_t* sX, const u
     a.errorProbability = errorProbability;
     a.maxIter = maxIter < 0 ? 0 : maxIter;
     a.stop = stop;
-    for (size_t k = 0; k < c.EX.size(); ++k) a.EX[k] = c.EX[k];
-    for (size_t k = 0; k < c.EZ.size(); ++k) a.EZ[k] = c.EZ[k];
-    const int wavesPerBlock = 4;
+    relabel(c.EX.data(), c.J, c.L, c.P, a.SX, a.DX, a.CX);
+    relabel(c.EZ.data(), c.K, c.L, c.P, a.SZ, a.DZ, a.CZ);
+    const int wavesPerBlock = QEC_WAVES_PER_BLOCK;
     const long long waves = (B + a.G - 1) / a.G;
     const long long blocks = (waves + wavesPerBlock - 1) / wavesPerBlock;
     if (blocks > 0x7fffffffLL) return fail(QEC_ERR_ARG, "batch too large for one launch");

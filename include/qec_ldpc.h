@@ -144,6 +144,38 @@ int qec_sample_fixed_weight(uint32_t seed, int W, size_t count, int n, uint8_t* 
 int qec_get_statistics(qec_decoder* dec, int errorWeight, int numErrors, float errorProbability,
                        int maxIterations, uint32_t seed, int nThreads, qec_stats* out);
 
+/* ---- Monte-Carlo on the device (the GetStatistics loop, batched) ---- */
+/* counters in device order for qec_statistics_dev */
+enum { QEC_MC_WITHX, QEC_MC_WITHZ, QEC_MC_SYNX, QEC_MC_SYNZ, QEC_MC_LOGICAL, QEC_MC_CORRECTED, QEC_MC_CONVX,
+       QEC_MC_CONVZ, QEC_MC_NCOUNTERS };
+
+typedef struct {
+    uint64_t tested, withX, withZ, synX, synZ, logical, corrected, convX, convZ;
+    uint64_t iterationsX, iterationsZ; /* BP iterations executed, summed over samples */
+    double decodeSeconds;             /* decode-kernel time (HIP events), summed over batches */
+    double totalSeconds;              /* wall time of the call */
+} qec_mc_result;
+
+/* i.i.d. depolarising errors for samples [start, start+B) of stream `seed` (device buffers
+ * x, z: B x n).  Philox4x32-10 with counter (sample lo, sample hi, qubit, 0x51EC0DE5) and key
+ * (seed lo, seed hi): the qubit is hit if word0 < floor(p 2^32); its type is (word1 * 3) >> 32
+ * (0 = X, 1 = Y, 2 = Z; Y sets both bits).  Any shard of the index space can be drawn alone. */
+int qec_sample_depolarizing_dev(qec_decoder* dec, uint64_t seed, uint64_t start, size_t B, float p, uint8_t* x,
+                                uint8_t* z, void* stream);
+/* GetSyndromeX/Z (Quantum_LDPC_Code.h:94-124) of device error vectors: x, z B x n -> sX B x numEqsX, sZ B x numEqsZ */
+int qec_syndrome_dev(qec_decoder* dec, const uint8_t* x, const uint8_t* z, size_t B, uint8_t* sX, uint8_t* sZ,
+                     void* stream);
+/* The CodeStatistics counters of a decoded device batch (DecoderCPU.h:464-521: errors present,
+ * syndrome fails, I-P logical check when neither syndrome failed, convergence fails), ADDED to
+ * the device array counters[QEC_MC_NCOUNTERS] (uint64). */
+int qec_statistics_dev(qec_decoder* dec, const uint8_t* x, const uint8_t* z, const uint8_t* eX, const uint8_t* eZ,
+                       const uint8_t* flags, size_t B, uint64_t* counters, void* stream);
+/* A whole Monte-Carlo run on the device: `count` depolarising samples from `start` of stream
+ * `seed`, in batches of `batch`: sample -> syndrome -> decode (stop rule `stop`) -> statistics.
+ * Synchronous; fills *out. */
+int qec_monte_carlo(qec_decoder* dec, uint64_t seed, uint64_t start, uint64_t count, float errorProbability,
+                    int maxIterations, int stop, size_t batch, qec_mc_result* out);
+
 #ifdef __cplusplus
 }
 #endif

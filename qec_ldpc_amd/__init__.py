@@ -34,7 +34,9 @@ EXPORTS = (
     "qec_decoder_create", "qec_decoder_destroy", "qec_decoder_describe",
     "qec_decode_batch", "qec_decode_batch_dev",
     "qec_sample_fixed_weight", "qec_get_statistics",
+    "qec_sample_depolarizing_dev", "qec_syndrome_dev", "qec_statistics_dev", "qec_monte_carlo",
 )
+MC_COUNTERS = ("withX", "withZ", "synX", "synZ", "logical", "corrected", "convX", "convZ")
 
 
 class QecError(RuntimeError):
@@ -52,6 +54,17 @@ class Stats(ctypes.Structure):
 
     def as_dict(self):
         return {k: int(getattr(self, k)) for k, _ in self._fields_}
+
+
+class MCResult(ctypes.Structure):
+    """qec_mc_result: a device Monte-Carlo run's counters and timings."""
+    _fields_ = [(k, ctypes.c_uint64) for k in ("tested", "withX", "withZ", "synX", "synZ", "logical", "corrected",
+                                               "convX", "convZ", "iterationsX", "iterationsZ")] + \
+               [("decodeSeconds", ctypes.c_double), ("totalSeconds", ctypes.c_double)]
+
+    def as_dict(self):
+        return {k: (float(getattr(self, k)) if t is ctypes.c_double else int(getattr(self, k)))
+                for k, t in self._fields_}
 
 
 _lib = None
@@ -84,6 +97,11 @@ def lib():
             "qec_decode_batch_dev": (i, [vp, vp, vp, sz, f, i, i, vp, vp, vp, vp, vp, vp]),
             "qec_sample_fixed_weight": (i, [ctypes.c_uint32, i, sz, i, vp, vp]),
             "qec_get_statistics": (i, [vp, i, i, f, i, ctypes.c_uint32, i, ctypes.POINTER(Stats)]),
+            "qec_sample_depolarizing_dev": (i, [vp, ctypes.c_uint64, ctypes.c_uint64, sz, f, vp, vp, vp]),
+            "qec_syndrome_dev": (i, [vp, vp, vp, sz, vp, vp, vp]),
+            "qec_statistics_dev": (i, [vp, vp, vp, vp, vp, vp, sz, vp, vp]),
+            "qec_monte_carlo": (i, [vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, f, i, i, sz,
+                                    ctypes.POINTER(MCResult)]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)
@@ -273,6 +291,37 @@ class DecoderGPU:
         _check(lib().qec_decode_batch_dev(self._h, addr(sX), addr(sZ), B, float(p), int(max_iter), STOP[stop],
                                           addr(eX), addr(eZ), addr(flags), addr(iters), addr(q),
                                           ctypes.c_void_p(stream)), "qec_decode_batch_dev")
+
+    @staticmethod
+    def _stream(stream):
+        if stream is None:
+            import torch
+            return torch.cuda.current_stream().cuda_stream
+        return stream if isinstance(stream, int) else stream.cuda_stream
+
+    def sample_depolarizing_dev(self, seed, start, p, x, z, stream=None):
+        """Device Philox depolarising errors for samples [start, start + x.shape[0])."""
+        _check(lib().qec_sample_depolarizing_dev(self._h, seed & (2 ** 64 - 1), start, x.shape[0], float(p),
+                                                 x.data_ptr(), z.data_ptr(), ctypes.c_void_p(self._stream(stream))),
+               "qec_sample_depolarizing_dev")
+
+    def syndrome_dev(self, x, z, sX, sZ, stream=None):
+        _check(lib().qec_syndrome_dev(self._h, x.data_ptr(), z.data_ptr(), x.shape[0], sX.data_ptr(), sZ.data_ptr(),
+                                      ctypes.c_void_p(self._stream(stream))), "qec_syndrome_dev")
+
+    def statistics_dev(self, x, z, eX, eZ, flags, counters, stream=None):
+        """Adds the batch's CodeStatistics counters into the int64 device tensor counters[8]
+        (order: MC_COUNTERS)."""
+        _check(lib().qec_statistics_dev(self._h, x.data_ptr(), z.data_ptr(), eX.data_ptr(), eZ.data_ptr(),
+                                        flags.data_ptr(), x.shape[0], counters.data_ptr(),
+                                        ctypes.c_void_p(self._stream(stream))), "qec_statistics_dev")
+
+    def monte_carlo(self, seed, start, count, p, max_iter, stop="syndrome", batch=65536):
+        """Device Monte-Carlo run (sample -> syndrome -> decode -> statistics); returns a dict."""
+        r = MCResult()
+        _check(lib().qec_monte_carlo(self._h, seed & (2 ** 64 - 1), start, count, float(p), int(max_iter),
+                                     STOP[stop], batch, ctypes.byref(r)), "qec_monte_carlo")
+        return r.as_dict()
 
     def Decode(self, syndromeX, syndromeZ, errorProbability, maxIterations):
         """Decoder::Decode for one syndrome pair -> (ErrorCode, outErrorsX, outErrorsZ)."""

@@ -5,6 +5,8 @@
 #include <cstring>
 #include <memory>
 #include <new>
+#include <stdexcept>
+#include <algorithm>
 
 #include "../../include/HostDeviceArray.h"
 #include "qec_internal.h"
@@ -15,6 +17,14 @@ const void* select_variant(const Code& c, std::string& name);
 int launch_decode(const void* variant, const Code& c, const uint8_t* sX, const uint8_t* sZ, long long B,
                   float errorProbability, int maxIter, int stop, uint8_t* eX, uint8_t* eZ, uint8_t* flags,
                   int32_t* iters, float* q, hipStream_t stream);
+int launch_sample_depolarizing(uint64_t seed, uint64_t start, long long B, int n, float p, uint8_t* x, uint8_t* z,
+                               hipStream_t st);
+int launch_errors_from_draws(const int32_t* idx, const uint8_t* type, long long B, int W, int n, uint8_t* x,
+                             uint8_t* z, hipStream_t st);
+int launch_syndrome(const Code& c, const uint8_t* x, const uint8_t* z, long long B, uint8_t* sX, uint8_t* sZ,
+                    hipStream_t st);
+int launch_statistics(const Code& c, const uint64_t* imp_dev, const uint8_t* x, const uint8_t* z, const uint8_t* eX,
+                      const uint8_t* eZ, const uint8_t* flags, long long B, unsigned long long* counters, hipStream_t st);
 }  // namespace qec
 
 using namespace qec;
@@ -33,6 +43,12 @@ struct qec_decoder {
     DeviceArray<uint8_t> sX, sZ, eX, eZ, flags;
     DeviceArray<int32_t> iters;
     DeviceArray<float> q;
+    // Monte-Carlo workspace (qec_monte_carlo / qec_get_statistics)
+    DeviceArray<uint64_t> imp;  // bit-packed non-zero I-P rows
+    DeviceArray<uint8_t> mx, mz, msX, msZ, meX, meZ, mfl, mtype;
+    DeviceArray<int32_t> mit, midx;
+    DeviceArray<unsigned long long> mcount;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
 };
 
 #define QEC_HIP_CHECK(expr)                                                                     \
@@ -150,6 +166,26 @@ qec_decoder* qec_decoder_create(const qec_code* h, int device, size_t max_batch)
         return nullptr;
     }
     (void)max_batch;  // staging grows on demand
+    try {
+        if (!d->code->imp_rows.empty()) {
+            d->imp.reserve(d->code->imp_rows.size());
+            if (hipMemcpy(d->imp.data(), d->code->imp_rows.data(), d->code->imp_rows.size() * sizeof(uint64_t),
+                          hipMemcpyHostToDevice) != hipSuccess)
+                throw std::runtime_error("I-P upload");
+        }
+        d->mcount.reserve(QEC_MC_NCOUNTERS);
+    } catch (const std::exception& ex) {
+        (void)hipStreamDestroy(d->stream);
+        delete d;
+        fail(QEC_ERR_HIP, std::string("qec_decoder_create: ") + ex.what());
+        return nullptr;
+    }
+    if (hipEventCreate(&d->ev0) != hipSuccess || hipEventCreate(&d->ev1) != hipSuccess) {
+        (void)hipStreamDestroy(d->stream);
+        delete d;
+        fail(QEC_ERR_HIP, "hipEventCreate failed");
+        return nullptr;
+    }
     return d;
 }
 
@@ -157,6 +193,8 @@ int qec_decoder_destroy(qec_decoder* d)
 {
     if (!d) return QEC_OK;
     (void)hipSetDevice(d->device);
+    if (d->ev0) (void)hipEventDestroy(d->ev0);
+    if (d->ev1) (void)hipEventDestroy(d->ev1);
     if (d->stream) (void)hipStreamDestroy(d->stream);
     delete d;
     return QEC_OK;
@@ -237,8 +275,42 @@ int qec_sample_fixed_weight(uint32_t seed, int W, size_t count, int n, uint8_t* 
     return QEC_OK;
 }
 
-// GetStatistics (DecoderCPU.h:392-530) with the decode batched on the GPU.  Errors are drawn
-// from the reference's stream in sample order; counters are order independent.
+static void mc_reserve(qec_decoder* d, size_t B, int W)
+{
+    const Code& c = *d->code;
+    d->mx.reserve(B * c.n); d->mz.reserve(B * c.n);
+    d->msX.reserve(B * c.mX); d->msZ.reserve(B * c.mZ);
+    d->meX.reserve(B * c.n); d->meZ.reserve(B * c.n);
+    d->mfl.reserve(B); d->mit.reserve(2 * B);
+    if (W > 0) { d->midx.reserve(B * W); d->mtype.reserve(B * W); }
+}
+
+// decode + statistics of the batch already in d->mx / d->mz; adds decode time
+static int mc_decode_and_count(qec_decoder* d, long long B, float p, int maxIter, int stop, double& decode_s)
+{
+    const Code& c = *d->code;
+    hipStream_t st = d->stream;
+    int rc = launch_syndrome(c, d->mx.data(), d->mz.data(), B, d->msX.data(), d->msZ.data(), st);
+    if (rc) return rc;
+    QEC_HIP_CHECK(hipEventRecord(d->ev0, st));
+    rc = launch_decode(d->variant, c, d->msX.data(), d->msZ.data(), B, p, maxIter, stop, d->meX.data(), d->meZ.data(),
+                       d->mfl.data(), d->mit.data(), nullptr, st);
+    if (rc) return rc;
+    QEC_HIP_CHECK(hipEventRecord(d->ev1, st));
+    rc = launch_statistics(c, d->imp.data(), d->mx.data(), d->mz.data(), d->meX.data(), d->meZ.data(), d->mfl.data(), B,
+                           d->mcount.data(), st);
+    if (rc) return rc;
+    QEC_HIP_CHECK(hipEventSynchronize(d->ev1));
+    float ms = 0;
+    QEC_HIP_CHECK(hipEventElapsedTime(&ms, d->ev0, d->ev1));
+    decode_s += ms * 1e-3;
+    return QEC_OK;
+}
+
+// GetStatistics (DecoderCPU.h:392-530).  The errors are the reference's: W (index, type) draws
+// per sample from one mt19937(seed) stream through VS2015's uniform_int_distribution, drawn on
+// the host in sample order (the stream is sequential).  Everything after the draws runs on the
+// GPU: error expansion, syndromes, decode (reference stop rule), I-P check, counters.
 int qec_get_statistics(qec_decoder* d, int W, int numErrors, float p, int maxIter, uint32_t seed, int nThreads,
                        qec_stats* out)
 {
@@ -246,63 +318,130 @@ int qec_get_statistics(qec_decoder* d, int W, int numErrors, float p, int maxIte
     const Code& c = *d->code;
     if (c.imp.empty()) return fail(QEC_ERR_UNSUPPORTED, "qec_get_statistics: code has no I-P matrix for the logical check");
     if (nThreads < 1) nThreads = 1;
+    QEC_HIP_CHECK(hipSetDevice(d->device));
     const auto t0 = std::chrono::high_resolution_clock::now();
     const long tested = (long)(numErrors / nThreads) * nThreads;  // DecoderCPU.h:426,527
     const long CH = 1 << 16;
     const int n = c.n;
-    std::vector<uint8_t> x, z, sx, sz, ex, ez, fl, res(n * 2);
+    hipStream_t st = d->stream;
+    try {
+        mc_reserve(d, (size_t)std::min<long>(CH, std::max<long>(tested, 1)), W);
+    } catch (const std::exception& ex) {
+        return fail(QEC_ERR_HIP, std::string("qec_get_statistics: ") + ex.what());
+    }
+    QEC_HIP_CHECK(hipMemsetAsync(d->mcount.data(), 0, QEC_MC_NCOUNTERS * sizeof(unsigned long long), st));
+    PinnedArray<int32_t> hidx;
+    PinnedArray<uint8_t> htype;
+    hidx.reserve((size_t)std::min<long>(CH, std::max<long>(tested, 1)) * std::max(W, 1));
+    htype.reserve((size_t)std::min<long>(CH, std::max<long>(tested, 1)) * std::max(W, 1));
     Mt19937 g(seed);
-    std::memset(out, 0, sizeof *out);
-    uint64_t withX = 0, withZ = 0, corrected = 0, synX = 0, synZ = 0, logical = 0, convX = 0, convZ = 0;
+    double dec_s = 0;
     for (long base = 0; base < tested; base += CH) {
         const long cnt = std::min(CH, tested - base);
-        x.assign((size_t)cnt * n, 0); z.assign((size_t)cnt * n, 0);
-        sx.resize((size_t)cnt * c.mX); sz.resize((size_t)cnt * c.mZ);
-        ex.resize((size_t)cnt * n); ez.resize((size_t)cnt * n); fl.resize(cnt);
         for (long s = 0; s < cnt; ++s)
             for (int w = 0; w < W; ++w) {
-                const uint32_t index = g.msvc_uniform((uint32_t)n);
-                const uint32_t type = g.msvc_uniform(3u);
-                if (type == 0 || type == 1) x[s * n + index] = 1;
-                if (type == 2 || type == 1) z[s * n + index] = 1;
+                hidx[s * W + w] = (int32_t)g.msvc_uniform((uint32_t)n);  // index, then type (DecoderCPU.h:452-454)
+                htype[s * W + w] = (uint8_t)g.msvc_uniform(3u);
             }
-        for (long s = 0; s < cnt; ++s) {
-            host_syndrome(c, 0, &x[s * n], &sx[s * c.mX]);
-            host_syndrome(c, 1, &z[s * n], &sz[s * c.mZ]);
+        if (W > 0) {
+            QEC_HIP_CHECK(hipMemcpyAsync(d->midx.data(), hidx.data(), (size_t)cnt * W * sizeof(int32_t),
+                                         hipMemcpyHostToDevice, st));
+            QEC_HIP_CHECK(hipMemcpyAsync(d->mtype.data(), htype.data(), (size_t)cnt * W, hipMemcpyHostToDevice, st));
         }
-        int rc = qec_decode_batch(d, sx.data(), sz.data(), cnt, p, maxIter, QEC_STOP_REF, ex.data(), ez.data(),
-                                  fl.data(), nullptr, nullptr);
+        int rc = launch_errors_from_draws(d->midx.data(), d->mtype.data(), cnt, W, n, d->mx.data(), d->mz.data(), st);
         if (rc) return rc;
-        for (long s = 0; s < cnt; ++s) {
-            bool ax = false, az = false;
-            for (int v = 0; v < n; ++v) { ax |= x[s * n + v] != 0; az |= z[s * n + v] != 0; }
-            withX += ax; withZ += az;
-            const bool dEX = fl[s] & QEC_SYNDROME_FAIL_X, dEZ = fl[s] & QEC_SYNDROME_FAIL_Z;
-            synX += dEX; synZ += dEZ;
-            if (!(dEX || dEZ)) {
-                for (int v = 0; v < n; ++v) {
-                    res[v] = (x[s * n + v] + ex[s * n + v]) % 2;
-                    res[n + v] = (z[s * n + v] + ez[s * n + v]) % 2;
-                }
-                if (host_check_logical(c, res.data(), res.data() + n)) ++logical; else ++corrected;
-            }
-            convX += (fl[s] & QEC_CONVERGENCE_FAIL_X) != 0;
-            convZ += (fl[s] & QEC_CONVERGENCE_FAIL_Z) != 0;
-        }
+        rc = mc_decode_and_count(d, cnt, p, maxIter, QEC_STOP_REF, dec_s);
+        if (rc) return rc;
     }
+    unsigned long long cn[QEC_MC_NCOUNTERS];
+    QEC_HIP_CHECK(hipMemcpyAsync(cn, d->mcount.data(), sizeof cn, hipMemcpyDeviceToHost, st));
+    QEC_HIP_CHECK(hipStreamSynchronize(st));
     const auto t1 = std::chrono::high_resolution_clock::now();
+    std::memset(out, 0, sizeof *out);
     out->randSeed = seed;
     out->numErrorsTested = (uint32_t)tested;
-    out->numXErrorsTested = (uint32_t)withX;
-    out->numZErrorsTested = (uint32_t)withZ;
+    out->numXErrorsTested = (uint32_t)cn[QEC_MC_WITHX];
+    out->numZErrorsTested = (uint32_t)cn[QEC_MC_WITHZ];
     out->errorWeight = (uint32_t)W;
-    out->corrected = (uint32_t)corrected;
-    out->syndromeErrorsX = (uint32_t)synX;
-    out->syndromeErrorsZ = (uint32_t)synZ;
-    out->logicalErrors = (uint32_t)logical;
-    out->convergenceFailX = (uint32_t)convX;
-    out->convergenceFailZ = (uint32_t)convZ;
+    out->corrected = (uint32_t)cn[QEC_MC_CORRECTED];
+    out->syndromeErrorsX = (uint32_t)cn[QEC_MC_SYNX];
+    out->syndromeErrorsZ = (uint32_t)cn[QEC_MC_SYNZ];
+    out->logicalErrors = (uint32_t)cn[QEC_MC_LOGICAL];
+    out->convergenceFailX = (uint32_t)cn[QEC_MC_CONVX];
+    out->convergenceFailZ = (uint32_t)cn[QEC_MC_CONVZ];
     out->durationMicroSeconds = std::chrono::duration_cast<std::chrono::microseconds>(t1 - t0).count();
+    return QEC_OK;
+}
+
+int qec_sample_depolarizing_dev(qec_decoder* d, uint64_t seed, uint64_t start, size_t B, float p, uint8_t* x,
+                                uint8_t* z, void* stream)
+{
+    if (!d || (B && (!x || !z))) return fail(QEC_ERR_ARG, "qec_sample_depolarizing_dev: bad argument");
+    QEC_HIP_CHECK(hipSetDevice(d->device));
+    return launch_sample_depolarizing(seed, start, (long long)B, d->code->n, p, x, z, static_cast<hipStream_t>(stream));
+}
+
+int qec_syndrome_dev(qec_decoder* d, const uint8_t* x, const uint8_t* z, size_t B, uint8_t* sX, uint8_t* sZ,
+                     void* stream)
+{
+    if (!d || (B && (!x || !z || !sX || !sZ))) return fail(QEC_ERR_ARG, "qec_syndrome_dev: bad argument");
+    QEC_HIP_CHECK(hipSetDevice(d->device));
+    return launch_syndrome(*d->code, x, z, (long long)B, sX, sZ, static_cast<hipStream_t>(stream));
+}
+
+int qec_statistics_dev(qec_decoder* d, const uint8_t* x, const uint8_t* z, const uint8_t* eX, const uint8_t* eZ,
+                       const uint8_t* flags, size_t B, uint64_t* counters, void* stream)
+{
+    if (!d || !counters || (B && (!x || !z || !eX || !eZ || !flags)))
+        return fail(QEC_ERR_ARG, "qec_statistics_dev: bad argument");
+    if (d->code->imp.empty()) return fail(QEC_ERR_UNSUPPORTED, "qec_statistics_dev: code has no I-P matrix");
+    QEC_HIP_CHECK(hipSetDevice(d->device));
+    return launch_statistics(*d->code, d->imp.data(), x, z, eX, eZ, flags, (long long)B,
+                             reinterpret_cast<unsigned long long*>(counters), static_cast<hipStream_t>(stream));
+}
+
+int qec_monte_carlo(qec_decoder* d, uint64_t seed, uint64_t start, uint64_t count, float p, int maxIter, int stop,
+                    size_t batch, qec_mc_result* out)
+{
+    if (!d || !out || (stop < QEC_STOP_REF || stop > QEC_STOP_SYNDROME)) return fail(QEC_ERR_ARG, "qec_monte_carlo: bad argument");
+    const Code& c = *d->code;
+    if (c.imp.empty()) return fail(QEC_ERR_UNSUPPORTED, "qec_monte_carlo: code has no I-P matrix for the logical check");
+    QEC_HIP_CHECK(hipSetDevice(d->device));
+    if (batch == 0) batch = 65536;
+    const auto t0 = std::chrono::high_resolution_clock::now();
+    try {
+        mc_reserve(d, (size_t)std::min<uint64_t>(batch, std::max<uint64_t>(count, 1)), 0);
+    } catch (const std::exception& ex) {
+        return fail(QEC_ERR_HIP, std::string("qec_monte_carlo: ") + ex.what());
+    }
+    hipStream_t st = d->stream;
+    QEC_HIP_CHECK(hipMemsetAsync(d->mcount.data(), 0, QEC_MC_NCOUNTERS * sizeof(unsigned long long), st));
+    double dec_s = 0;
+    uint64_t itx = 0, itz = 0;
+    std::vector<int32_t> hit;
+    for (uint64_t base = 0; base < count; base += batch) {
+        const long long cnt = (long long)std::min<uint64_t>(batch, count - base);
+        int rc = launch_sample_depolarizing(seed, start + base, cnt, c.n, p, d->mx.data(), d->mz.data(), st);
+        if (rc) return rc;
+        rc = mc_decode_and_count(d, cnt, p, maxIter, stop, dec_s);
+        if (rc) return rc;
+        hit.resize(2 * (size_t)cnt);
+        QEC_HIP_CHECK(hipMemcpyAsync(hit.data(), d->mit.data(), hit.size() * sizeof(int32_t), hipMemcpyDeviceToHost, st));
+        QEC_HIP_CHECK(hipStreamSynchronize(st));
+        for (long long k = 0; k < cnt; ++k) { itx += hit[2 * k]; itz += hit[2 * k + 1]; }
+    }
+    unsigned long long cn[QEC_MC_NCOUNTERS];
+    QEC_HIP_CHECK(hipMemcpyAsync(cn, d->mcount.data(), sizeof cn, hipMemcpyDeviceToHost, st));
+    QEC_HIP_CHECK(hipStreamSynchronize(st));
+    const auto t1 = std::chrono::high_resolution_clock::now();
+    out->tested = count;
+    out->withX = cn[QEC_MC_WITHX]; out->withZ = cn[QEC_MC_WITHZ];
+    out->synX = cn[QEC_MC_SYNX]; out->synZ = cn[QEC_MC_SYNZ];
+    out->logical = cn[QEC_MC_LOGICAL]; out->corrected = cn[QEC_MC_CORRECTED];
+    out->convX = cn[QEC_MC_CONVX]; out->convZ = cn[QEC_MC_CONVZ];
+    out->iterationsX = itx; out->iterationsZ = itz;
+    out->decodeSeconds = dec_s;
+    out->totalSeconds = std::chrono::duration<double>(t1 - t0).count();
     return QEC_OK;
 }
 

@@ -1,0 +1,109 @@
+"""Device Monte-Carlo caller against the oracle:
+Philox sampler vs its numpy restatement, circulant syndrome kernel vs the host
+code model, statistics kernel and whole qec_monte_carlo runs vs counting with the
+oracle's decoder and I-P check (DecoderCPU.h:464-521) on the same samples."""
+import numpy as np
+import pytest
+import torch
+
+import qec_ldpc_amd as q
+from oracle.oracle import OracleCode
+from oracle.philox import depolarizing
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda", 0)
+
+
+@pytest.fixture(scope="module")
+def env(code_paths):
+    out = {}
+    for k, path in code_paths.items():
+        code = q.Quantum_LDPC_Code.createFromFile(path)
+        out[k] = (code, q.DecoderGPU(code, 0), OracleCode(path))
+    return out
+
+
+def dev_u8(*shape):
+    return torch.empty(shape, dtype=torch.uint8, device=DEV)
+
+
+@pytest.mark.parametrize("key", ["P7", "P61"])
+@pytest.mark.parametrize("seed,start,p", [(0x51EC0DE, 0, 0.01), (12345, (1 << 32) - 3, 0.2), (7, 99, 0.0),
+                                          (7, 5, 1.0), (2 ** 63 + 5, 1 << 40, 0.05)])
+def test_sampler_matches_numpy(env, key, seed, start, p):
+    code, dec, _ = env[key]
+    B = 300
+    x, z = dev_u8(B, code.n), dev_u8(B, code.n)
+    dec.sample_depolarizing_dev(seed, start, p, x, z)
+    torch.cuda.synchronize()
+    rx, rz = depolarizing(seed, start, B, code.n, p)
+    assert np.array_equal(x.cpu().numpy(), rx) and np.array_equal(z.cpu().numpy(), rz)
+
+
+@pytest.mark.parametrize("key", ["P7", "P61"])
+def test_syndrome_kernel(env, key):
+    code, dec, _ = env[key]
+    rng = np.random.default_rng(4)
+    ex = (rng.random((700, code.n)) < 0.05).astype(np.uint8)
+    ez = (rng.random((700, code.n)) < 0.05).astype(np.uint8)
+    sX, sZ = dev_u8(700, code.numEqsX), dev_u8(700, code.numEqsZ)
+    dec.syndrome_dev(torch.from_numpy(ex).to(DEV), torch.from_numpy(ez).to(DEV), sX, sZ)
+    torch.cuda.synchronize()
+    assert np.array_equal(sX.cpu().numpy(), code.syndrome(0, ex))
+    assert np.array_equal(sZ.cpu().numpy(), code.syndrome(1, ez))
+
+
+def oracle_counters(orc, x, z, p, N, stop):
+    sx, sz = orc.syndrome(0, x), orc.syndrome(1, z)
+    eX, eZ, fl, it, _ = orc.decode_batch(sx, sz, p, N, stop)
+    c = dict.fromkeys(q.MC_COUNTERS, 0)
+    c["withX"] = int(x.any(1).sum())
+    c["withZ"] = int(z.any(1).sum())
+    c["synX"] = int((fl & 1 != 0).sum())
+    c["synZ"] = int((fl & 2 != 0).sum())
+    c["convX"] = int((fl & 4 != 0).sum())
+    c["convZ"] = int((fl & 8 != 0).sum())
+    for b in np.nonzero((fl & 3) == 0)[0]:
+        if orc.check_logical(x[b] ^ eX[b], z[b] ^ eZ[b]):
+            c["logical"] += 1
+        else:
+            c["corrected"] += 1
+    return c, it
+
+
+@pytest.mark.parametrize("key,B,p,N", [("P7", 4000, 0.06, 30), ("P61", 300, 0.03, 30)])
+def test_statistics_kernel_matches_oracle(env, key, B, p, N):
+    code, dec, orc = env[key]
+    x, z = depolarizing(99, 0, B, code.n, p)
+    xd, zd = torch.from_numpy(x).to(DEV), torch.from_numpy(z).to(DEV)
+    sX, sZ = dev_u8(B, code.numEqsX), dev_u8(B, code.numEqsZ)
+    dec.syndrome_dev(xd, zd, sX, sZ)
+    eX, eZ, fl = dev_u8(B, code.n), dev_u8(B, code.n), dev_u8(B)
+    dec.decode_batch_dev(sX, sZ, p, N, "ref", eX, eZ, fl)
+    cnt = torch.zeros(8, dtype=torch.int64, device=DEV)
+    dec.statistics_dev(xd, zd, eX, eZ, fl, cnt)
+    torch.cuda.synchronize()
+    got = dict(zip(q.MC_COUNTERS, cnt.cpu().tolist()))
+    exp, _ = oracle_counters(orc, x, z, p, N, "ref")
+    assert got == exp
+
+
+@pytest.mark.parametrize("stop", ["ref", "syndrome", "fixed"])
+@pytest.mark.parametrize("key,count,p", [("P7", 5000, 0.05), ("P61", 400, 0.04)])
+def test_monte_carlo_matches_oracle(env, key, count, p, stop):
+    code, dec, orc = env[key]
+    r = dec.monte_carlo(0xBEEF, 17, count, p, 25, stop, batch=1000)
+    x, z = depolarizing(0xBEEF, 17, count, code.n, p)
+    exp, it = oracle_counters(orc, x, z, p, 25, stop)
+    assert {k: r[k] for k in q.MC_COUNTERS} == exp
+    assert r["tested"] == count
+    assert r["iterationsX"] == int(it[:, 0].sum()) and r["iterationsZ"] == int(it[:, 1].sum())
+
+
+def test_monte_carlo_shards_add_up(env):
+    code, dec, _ = env["P61"]
+    whole = dec.monte_carlo(5, 0, 6000, 0.03, 50, "syndrome", batch=2048)
+    a = dec.monte_carlo(5, 0, 2500, 0.03, 50, "syndrome", batch=4096)
+    b = dec.monte_carlo(5, 2500, 3500, 0.03, 50, "syndrome", batch=777)
+    for k in q.MC_COUNTERS + ("tested", "iterationsX", "iterationsZ"):
+        assert whole[k] == a[k] + b[k], k

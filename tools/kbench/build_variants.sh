@@ -11,6 +11,7 @@ build() {
   mkdir -p $out
   $HIPCC $BASE "$@" -c qec_ldpc_amd/csrc/bp_decode.hip -o $out/bp_decode.o &
   $HIPCC $BASE -x c++ -c qec_ldpc_amd/csrc/code_model.cpp -o $out/code_model.o &
+  $HIPCC $BASE -c qec_ldpc_amd/csrc/montecarlo.hip -o $out/montecarlo.o &
   $HIPCC $BASE -x hip -c qec_ldpc_amd/csrc/capi.cpp -o $out/capi.o &
   wait
   $HIPCC --offload-arch=gfx950 -shared -fPIC -o $out/libqecldpc.so $out/*.o

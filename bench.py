@@ -35,6 +35,7 @@ CODES = {
     "p7": ("J_3_K_3_L_6_P_7_s_2_t_3", 0.02, 20,
            "BASELINE configs[1]: J=3,K=3,L=6,P=7 code, batch 65536 per GPU, 20 fixed BP iters"),
 }
+SEED = 0x51EC0DE
 HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md, chip-level parameters
 VALU_PEAK_TOPS = 78.64          # 256 CU x 4 SIMD x 32 lanes x 2.4 GHz lane-ops/s (fp32 non-FMA issue ceiling)
 
@@ -82,7 +83,6 @@ def main():
 
     import qec_ldpc_amd as q
     from qec_ldpc_amd.codes import code_path
-    from qec_ldpc_amd.synthetic import depolarizing_errors
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -99,11 +99,16 @@ def main():
     dec = q.DecoderGPU(code, local)
     B = args.batch
 
-    # rank's shard of the sample index space: [rank*B, (rank+1)*B)
-    x, z = depolarizing_errors(code.n, rank * B, B, p)
-    sX_h, sZ_h = code.syndrome(0, x), code.syndrome(1, z)
-    sX = torch.from_numpy(sX_h).to(dev)
-    sZ = torch.from_numpy(sZ_h).to(dev)
+    # rank's shard of the sample index space, [rank*B, (rank+1)*B), drawn on the device
+    # (Philox depolarising sampler + circulant syndrome kernel) before the timed region
+    x = torch.empty((B, code.n), dtype=torch.uint8, device=dev)
+    z = torch.empty((B, code.n), dtype=torch.uint8, device=dev)
+    sX = torch.empty((B, code.numEqsX), dtype=torch.uint8, device=dev)
+    sZ = torch.empty((B, code.numEqsZ), dtype=torch.uint8, device=dev)
+    dec.sample_depolarizing_dev(SEED, rank * B, p, x, z)
+    dec.syndrome_dev(x, z, sX, sZ)
+    torch.cuda.synchronize(dev)
+    del x, z
     eX = torch.empty((B, code.n), dtype=torch.uint8, device=dev)
     eZ = torch.empty((B, code.n), dtype=torch.uint8, device=dev)
     fl = torch.empty(B, dtype=torch.uint8, device=dev)
@@ -172,7 +177,8 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f32",
-        "data": "synthetic i.i.d. depolarising errors (Philox, seed 0x51EC0DE), syndromes resident in HBM",
+        "data": "synthetic i.i.d. depolarising errors (device Philox4x32-10 sampler, seed 0x51EC0DE), "
+                "syndromes resident in HBM",
         "config": {"workload": label if world == 1 else label + " (BASELINE configs[3] shape, sharded)",
                    "code": code.describe(), "global_batch": B * world, "per_gpu_batch": B,
                    "bp_iters": iters, "stop": args.stop, "p": p, "parallelism": "dp%d" % world,
@@ -188,7 +194,7 @@ def main():
         out["iteration_histogram"] = {str(k): int(v) for k, v in enumerate(hist) if v}
 
     if rank == 0 and world == 1 and not args.no_cpu:
-        out["cpu_baseline"] = cpu_baseline(code, fname, sX_h, sZ_h, p, iters, args, eX, eZ, fl)
+        out["cpu_baseline"] = cpu_baseline(code, fname, sX.cpu().numpy(), sZ.cpu().numpy(), p, iters, args, eX, eZ, fl)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

@@ -1,0 +1,104 @@
+"""Physical error-rate sweep (BASELINE.json configs[4]): P61 code, early-termination
+BP (--stop syndrome: stop once the hard decision satisfies the syndrome, cap 50
+iterations), i.i.d. depolarising errors, on N GPUs.
+
+One process per GPU (python -m torch.distributed.run --nproc-per-node N
+tools/psweep.py ...).  Each rank runs qec_monte_carlo on its contiguous shard of
+the sample index space (device sampler -> syndromes -> decode -> I-P check ->
+counters, all on its GPU); the per-p counters are summed across ranks with one
+all-reduce (RCCL over xGMI) and the wall time is the max over ranks.  Rank 0
+prints one JSON line per p and a final summary line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+DEFAULT_PS = [1e-3, 2e-3, 5e-3, 1e-2, 2e-2, 5e-2, 1e-1]
+FIELDS = ("tested", "withX", "withZ", "synX", "synZ", "logical", "corrected", "convX", "convZ", "iterationsX",
+          "iterationsZ")
+
+
+def summarize(p, c, seconds, world):
+    """Rates from summed counters (also used by the CPU test of the reduction)."""
+    t = max(c["tested"], 1)
+    failed = c["tested"] - c["corrected"]
+    return {
+        "p": p, "samples": c["tested"], "n_gpus": world,
+        "syndromes_per_s": round(c["tested"] / seconds, 1) if seconds > 0 else None,
+        "seconds": round(seconds, 4),
+        "logical_error_rate": c["logical"] / t,
+        "decoder_failure_rate": failed / t,  # syndrome fail or logical error
+        "syndrome_fail_rate_x": c["synX"] / t, "syndrome_fail_rate_z": c["synZ"] / t,
+        "mean_iterations_x": c["iterationsX"] / t, "mean_iterations_z": c["iterationsZ"] / t,
+        "counters": {k: int(c[k]) for k in FIELDS},
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--code", default="J_4_K_5_L_10_P_61_s_9_t_49")
+    ap.add_argument("--total", type=int, default=1 << 20, help="samples per p over all GPUs")
+    ap.add_argument("--ps", type=float, nargs="*", default=DEFAULT_PS)
+    ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--stop", default="syndrome", choices=["syndrome", "ref", "fixed"])
+    ap.add_argument("--batch", type=int, default=65536)
+    ap.add_argument("--seed", type=lambda v: int(v, 0), default=0x51EC0DE)
+    ap.add_argument("--out", default=None, help="write the per-p lines to this JSON file (rank 0)")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    import qec_ldpc_amd as q
+    from qec_ldpc_amd.codes import code_path
+    from qec_ldpc_amd.synthetic import shard_range
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    code = q.Quantum_LDPC_Code.createFromFile(code_path(args.code))
+    dec = q.DecoderGPU(code, local)
+    lo, hi = shard_range(args.total, rank, world)
+    dec.monte_carlo(args.seed, lo, min(hi - lo, 4096), args.ps[0], args.iters, args.stop, args.batch)  # warm-up
+    lines = []
+    for p in args.ps:
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        r = dec.monte_carlo(args.seed, lo, hi - lo, p, args.iters, args.stop, args.batch)
+        dt = time.perf_counter() - t0
+        vec = torch.tensor([r[k] for k in FIELDS], dtype=torch.int64, device=dev)
+        tm = torch.tensor([dt], dtype=torch.float64, device=dev)
+        if world > 1:
+            dist.all_reduce(vec)
+            dist.all_reduce(tm, op=dist.ReduceOp.MAX)
+        c = dict(zip(FIELDS, vec.cpu().tolist()))
+        line = summarize(p, c, float(tm.item()), world)
+        line.update({"code": code.describe(), "stop": args.stop, "max_iters": args.iters, "seed": args.seed})
+        lines.append(line)
+        if rank == 0:
+            print(json.dumps(line), flush=True)
+    if rank == 0:
+        tot = sum(l["samples"] for l in lines)
+        sec = sum(l["seconds"] for l in lines)
+        print(json.dumps({"sweep": "psweep", "n_gpus": world, "total_samples": tot, "seconds": round(sec, 3),
+                          "syndromes_per_s": round(tot / sec, 1)}), flush=True)
+        if args.out:
+            with open(args.out, "w") as f:
+                json.dump(lines, f, indent=1)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

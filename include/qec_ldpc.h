@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define QEC_LDPC_ABI_VERSION 1
+#define QEC_LDPC_ABI_VERSION 2
 
 /* status codes */
 enum {
@@ -56,6 +56,13 @@ enum {
 };
 
 enum { QEC_SECTOR_X = 0, QEC_SECTOR_Z = 1 };
+
+/* GPU engines behind one decoder handle */
+enum {
+    QEC_ENGINE_AUTO = 0,       /* wave-circulant if the code has an instantiated kernel, else sparse-graph */
+    QEC_ENGINE_CIRCULANT = 1,  /* wave-circulant: circulant-permutation QC codes, P <= 64 (bp_decode.hip) */
+    QEC_ENGINE_SPARSE = 2      /* sparse-graph: any code DecoderCPU accepts (regular, dc = L, dv = J / K) */
+};
 
 typedef struct qec_code qec_code;
 typedef struct qec_decoder qec_decoder;
@@ -109,6 +116,11 @@ int qec_code_check_logical(const qec_code* code, const uint8_t* ex, const uint8_
  * device ordinal (>= 0; there is no CPU engine in the product).  max_batch sizes
  * the host-pointer staging buffers (grown on demand). */
 qec_decoder* qec_decoder_create(const qec_code* code, int device, size_t max_batch);
+/* Same with an explicit engine (QEC_ENGINE_*).  QEC_ENGINE_CIRCULANT fails with
+ * QEC_ERR_UNSUPPORTED when the code has no wave-circulant kernel; QEC_ENGINE_SPARSE fails
+ * for an irregular code (DecoderCPU's index tables assume row weight L and column weight
+ * J / K, DecoderCPU.h:41-84). */
+qec_decoder* qec_decoder_create_engine(const qec_code* code, int device, size_t max_batch, int engine);
 int qec_decoder_destroy(qec_decoder* dec);
 /* which kernel variant serves this code: writes a short name (e.g. "wave-circulant P=61 G=1") */
 int qec_decoder_describe(const qec_decoder* dec, char* buf, size_t len);

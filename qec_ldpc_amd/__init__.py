@@ -25,13 +25,14 @@ SYNDROME_FAIL_Z = 2
 CONVERGENCE_FAIL_X = 4
 CONVERGENCE_FAIL_Z = 8
 STOP = {"ref": 0, "fixed": 1, "syndrome": 2}
+ENGINE = {"auto": 0, "circulant": 1, "sparse": 2}
 
 # every symbol include/qec_ldpc.h declares
 EXPORTS = (
     "qec_last_error", "qec_abi_version",
     "qec_code_load", "qec_code_generate", "qec_code_free", "qec_code_params", "qec_code_exponents",
     "qec_code_pcm", "qec_code_describe", "qec_code_syndrome", "qec_code_check_logical",
-    "qec_decoder_create", "qec_decoder_destroy", "qec_decoder_describe",
+    "qec_decoder_create", "qec_decoder_create_engine", "qec_decoder_destroy", "qec_decoder_describe",
     "qec_decode_batch", "qec_decode_batch_dev",
     "qec_sample_fixed_weight", "qec_get_statistics",
     "qec_sample_depolarizing_dev", "qec_syndrome_dev", "qec_statistics_dev", "qec_monte_carlo",
@@ -91,6 +92,7 @@ def lib():
             "qec_code_syndrome": (i, [vp, i, vp, sz, vp]),
             "qec_code_check_logical": (i, [vp, vp, vp, sz, vp]),
             "qec_decoder_create": (vp, [vp, i, sz]),
+            "qec_decoder_create_engine": (vp, [vp, i, sz, i]),
             "qec_decoder_destroy": (i, [vp]),
             "qec_decoder_describe": (i, [vp, ctypes.c_char_p, sz]),
             "qec_decode_batch": (i, [vp, vp, vp, sz, f, i, i, vp, vp, vp, vp, vp]),
@@ -236,11 +238,14 @@ def sample_fixed_weight(seed, W, count, n):
 
 
 class DecoderGPU:
-    """MI355X BP engine behind the reference's DecoderGPU slot (QEC_LDPC/DecoderGPU.h)."""
+    """MI355X BP engine behind the reference's DecoderGPU slot (QEC_LDPC/DecoderGPU.h).
 
-    def __init__(self, code, device=0):
+    engine: "auto" (wave-circulant kernel when the code has one, else sparse-graph),
+    "circulant" or "sparse" (include/qec_ldpc.h, QEC_ENGINE_*)."""
+
+    def __init__(self, code, device=0, engine="auto"):
         self.code = code
-        h = lib().qec_decoder_create(code.handle, int(device), 0)
+        h = lib().qec_decoder_create_engine(code.handle, int(device), 0, ENGINE[engine])
         if not h:
             raise QecError(last_error())
         self._h = ctypes.c_void_p(h)

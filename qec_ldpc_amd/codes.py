@@ -25,3 +25,23 @@ def code_path(name):
         g.write(f.read())
     _cache[name] = dst
     return dst
+
+
+def write_code_file(path, J, K, L, P, sigma, tau, HX, HZ, IMP=None):
+    """Write a code in the reference's 4-line text format (Quantum_LDPC_Code.h:26-80):
+    "J K L P sigma tau" / HX row-major / HZ row-major / I-P row-major (zeros if None)."""
+    import numpy as np
+
+    n = HX.shape[1]
+    if IMP is None:
+        IMP = np.zeros((2 * n, 2 * n), dtype=np.uint8)
+
+    def row(a):
+        return " ".join(map(str, np.asarray(a, dtype=np.uint8).ravel().tolist()))
+
+    with open(path, "w") as f:
+        f.write("%d %d %d %d %d %d\n" % (J, K, L, P, sigma, tau))
+        f.write(row(HX) + "\n")
+        f.write(row(HZ) + "\n")
+        f.write(row(IMP) + "\n")
+    return path

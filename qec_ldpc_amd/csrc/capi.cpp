@@ -21,8 +21,15 @@ int launch_sample_depolarizing(uint64_t seed, uint64_t start, long long B, int n
                                hipStream_t st);
 int launch_errors_from_draws(const int32_t* idx, const uint8_t* type, long long B, int W, int n, uint8_t* x,
                              uint8_t* z, hipStream_t st);
-int launch_syndrome(const Code& c, const uint8_t* x, const uint8_t* z, long long B, uint8_t* sX, uint8_t* sZ,
-                    hipStream_t st);
+int launch_syndrome(const Code& c, const int32_t* chkVar, const uint8_t* x, const uint8_t* z, long long B,
+                    uint8_t* sX, uint8_t* sZ, hipStream_t st);
+void* sparse_plan_create(const Code& c, int device);
+void sparse_plan_free(void* plan);
+const char* sparse_plan_name(const void* plan);
+const int32_t* sparse_plan_chkvar(const void* plan);
+int launch_decode_sparse(void* plan, const uint8_t* sX, const uint8_t* sZ, long long B, float errorProbability,
+                         int maxIter, int stop, uint8_t* eX, uint8_t* eZ, uint8_t* flags, int32_t* iters, float* q,
+                         hipStream_t stream);
 int launch_statistics(const Code& c, const uint64_t* imp_dev, const uint8_t* x, const uint8_t* z, const uint8_t* eX,
                       const uint8_t* eZ, const uint8_t* flags, long long B, unsigned long long* counters, hipStream_t st);
 }  // namespace qec
@@ -36,7 +43,9 @@ struct qec_code {
 struct qec_decoder {
     std::shared_ptr<const Code> code;
     int device = 0;
-    const void* variant = nullptr;
+    int engine = QEC_ENGINE_CIRCULANT;
+    const void* variant = nullptr;  // wave-circulant kernel variant (bp_decode.hip)
+    void* sparse = nullptr;         // sparse-graph plan (bp_sparse.hip)
     std::string variant_name;
     hipStream_t stream = nullptr;
     // staging for the host-pointer entry point (DecoderGPU's device vectors, DecoderGPU.h:28-35)
@@ -138,12 +147,21 @@ int qec_code_check_logical(const qec_code* h, const uint8_t* ex, const uint8_t* 
 
 qec_decoder* qec_decoder_create(const qec_code* h, int device, size_t max_batch)
 {
+    return qec_decoder_create_engine(h, device, max_batch, QEC_ENGINE_AUTO);
+}
+
+qec_decoder* qec_decoder_create_engine(const qec_code* h, int device, size_t max_batch, int engine)
+{
     if (!h) { fail(QEC_ERR_ARG, "qec_decoder_create: null code"); return nullptr; }
     if (device < 0) { fail(QEC_ERR_ARG, "qec_decoder_create: the product has no CPU engine; device must be >= 0"); return nullptr; }
+    if (engine < QEC_ENGINE_AUTO || engine > QEC_ENGINE_SPARSE) {
+        fail(QEC_ERR_ARG, "qec_decoder_create_engine: unknown engine");
+        return nullptr;
+    }
     std::string name;
-    const void* v = select_variant(h->c, name);
-    if (!v) {
-        fail(QEC_ERR_UNSUPPORTED, "no GPU kernel for this code shape (" + h->c.describe() +
+    const void* v = engine == QEC_ENGINE_SPARSE ? nullptr : select_variant(h->c, name);
+    if (!v && engine == QEC_ENGINE_CIRCULANT) {
+        fail(QEC_ERR_UNSUPPORTED, "no wave-circulant kernel for this code shape (" + h->c.describe() +
                                       "): needs circulant-permutation blocks, P <= 64 and an instantiated (J,K,L)");
         return nullptr;
     }
@@ -160,6 +178,12 @@ qec_decoder* qec_decoder_create(const qec_code* h, int device, size_t max_batch)
     d->device = device;
     d->variant = v;
     d->variant_name = name;
+    if (!v) {  // AUTO without a wave-circulant kernel, or SPARSE requested
+        d->engine = QEC_ENGINE_SPARSE;
+        d->sparse = sparse_plan_create(*d->code, device);
+        if (!d->sparse) { delete d; return nullptr; }  // error text set by the plan
+        d->variant_name = sparse_plan_name(d->sparse);
+    }
     if (hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking) != hipSuccess) {
         delete d;
         fail(QEC_ERR_HIP, "hipStreamCreate failed");
@@ -196,6 +220,7 @@ int qec_decoder_destroy(qec_decoder* d)
     if (d->ev0) (void)hipEventDestroy(d->ev0);
     if (d->ev1) (void)hipEventDestroy(d->ev1);
     if (d->stream) (void)hipStreamDestroy(d->stream);
+    if (d->sparse) sparse_plan_free(d->sparse);
     delete d;
     return QEC_OK;
 }
@@ -205,6 +230,19 @@ int qec_decoder_describe(const qec_decoder* d, char* buf, size_t len)
     if (!d || !buf || !len) return fail(QEC_ERR_ARG, "qec_decoder_describe: bad argument");
     std::snprintf(buf, len, "%s", d->variant_name.c_str());
     return QEC_OK;
+}
+
+static int dispatch_decode(qec_decoder* d, const uint8_t* sX, const uint8_t* sZ, long long B, float p, int maxIter,
+                           int stop, uint8_t* eX, uint8_t* eZ, uint8_t* flags, int32_t* iters, float* q, hipStream_t st)
+{
+    if (d->engine == QEC_ENGINE_SPARSE)
+        return launch_decode_sparse(d->sparse, sX, sZ, B, p, maxIter, stop, eX, eZ, flags, iters, q, st);
+    return launch_decode(d->variant, *d->code, sX, sZ, B, p, maxIter, stop, eX, eZ, flags, iters, q, st);
+}
+
+static const int32_t* syndrome_table(const qec_decoder* d)
+{
+    return d->engine == QEC_ENGINE_SPARSE ? sparse_plan_chkvar(d->sparse) : nullptr;
 }
 
 static int check_decode_args(const qec_decoder* d, const void* sX, const void* sZ, size_t B, int stop,
@@ -223,8 +261,8 @@ int qec_decode_batch_dev(qec_decoder* d, const uint8_t* sX, const uint8_t* sZ, s
     int rc = check_decode_args(d, sX, sZ, B, stop, eX, eZ, flags);
     if (rc) return rc;
     QEC_HIP_CHECK(hipSetDevice(d->device));
-    return launch_decode(d->variant, *d->code, sX, sZ, (long long)B, p, maxIter, stop, eX, eZ, flags, iters, q,
-                         static_cast<hipStream_t>(stream));
+    return dispatch_decode(d, sX, sZ, (long long)B, p, maxIter, stop, eX, eZ, flags, iters, q,
+                           static_cast<hipStream_t>(stream));
 }
 
 int qec_decode_batch(qec_decoder* d, const uint8_t* sX, const uint8_t* sZ, size_t B, float p, int maxIter, int stop,
@@ -247,7 +285,7 @@ int qec_decode_batch(qec_decoder* d, const uint8_t* sX, const uint8_t* sZ, size_
     hipStream_t st = d->stream;
     QEC_HIP_CHECK(hipMemcpyAsync(d->sX.data(), sX, B * c.mX, hipMemcpyHostToDevice, st));
     QEC_HIP_CHECK(hipMemcpyAsync(d->sZ.data(), sZ, B * c.mZ, hipMemcpyHostToDevice, st));
-    rc = launch_decode(d->variant, c, d->sX.data(), d->sZ.data(), (long long)B, p, maxIter, stop, d->eX.data(),
+    rc = dispatch_decode(d, d->sX.data(), d->sZ.data(), (long long)B, p, maxIter, stop, d->eX.data(),
                        d->eZ.data(), d->flags.data(), iters ? d->iters.data() : nullptr, q ? d->q.data() : nullptr, st);
     if (rc) return rc;
     QEC_HIP_CHECK(hipMemcpyAsync(eX, d->eX.data(), B * c.n, hipMemcpyDeviceToHost, st));
@@ -290,10 +328,10 @@ static int mc_decode_and_count(qec_decoder* d, long long B, float p, int maxIter
 {
     const Code& c = *d->code;
     hipStream_t st = d->stream;
-    int rc = launch_syndrome(c, d->mx.data(), d->mz.data(), B, d->msX.data(), d->msZ.data(), st);
+    int rc = launch_syndrome(c, syndrome_table(d), d->mx.data(), d->mz.data(), B, d->msX.data(), d->msZ.data(), st);
     if (rc) return rc;
     QEC_HIP_CHECK(hipEventRecord(d->ev0, st));
-    rc = launch_decode(d->variant, c, d->msX.data(), d->msZ.data(), B, p, maxIter, stop, d->meX.data(), d->meZ.data(),
+    rc = dispatch_decode(d, d->msX.data(), d->msZ.data(), B, p, maxIter, stop, d->meX.data(), d->meZ.data(),
                        d->mfl.data(), d->mit.data(), nullptr, st);
     if (rc) return rc;
     QEC_HIP_CHECK(hipEventRecord(d->ev1, st));
@@ -386,7 +424,7 @@ int qec_syndrome_dev(qec_decoder* d, const uint8_t* x, const uint8_t* z, size_t 
 {
     if (!d || (B && (!x || !z || !sX || !sZ))) return fail(QEC_ERR_ARG, "qec_syndrome_dev: bad argument");
     QEC_HIP_CHECK(hipSetDevice(d->device));
-    return launch_syndrome(*d->code, x, z, (long long)B, sX, sZ, static_cast<hipStream_t>(stream));
+    return launch_syndrome(*d->code, syndrome_table(d), x, z, (long long)B, sX, sZ, static_cast<hipStream_t>(stream));
 }
 
 int qec_statistics_dev(qec_decoder* d, const uint8_t* x, const uint8_t* z, const uint8_t* eX, const uint8_t* eZ,

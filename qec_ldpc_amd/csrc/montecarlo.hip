@@ -105,6 +105,25 @@ __global__ void syndrome_kernel(const SynArgs a)
     (zs ? a.sZ : a.sX)[b * (zs ? a.mZ : a.mX) + c] = (uint8_t)s;
 }
 
+// Any regular code (sparse-graph engine): s(c) = XOR_k e[chkVar[c dc + k]], the check's
+// variables from the engine's InitIndexArrays table; one thread per (sample, check).
+__global__ void syndrome_csr_kernel(const uint8_t* __restrict__ x, const uint8_t* __restrict__ z,
+                                    const int32_t* __restrict__ chkVar, long long B, int n, int mX, int mZ, int dc,
+                                    uint8_t* __restrict__ sX, uint8_t* __restrict__ sZ)
+{
+    const int m = mX + mZ;
+    const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= B * m) return;
+    const long long b = t / m;
+    const int c = (int)(t - b * m);
+    const bool zs = c >= mX;
+    const uint8_t* e = (zs ? z : x) + b * n;
+    const int32_t* vars = chkVar + (size_t)c * dc;
+    uint32_t s = 0;
+    for (int k = 0; k < dc; ++k) s ^= e[vars[k]] & 1u;
+    if (zs) sZ[b * mZ + (c - mX)] = (uint8_t)s; else sX[b * mX + c] = (uint8_t)s;
+}
+
 // counters, in qec_mc_counters order
 enum { C_WITHX, C_WITHZ, C_SYNX, C_SYNZ, C_LOGICAL, C_CORRECTED, C_CONVX, C_CONVZ, C_N };
 
@@ -206,10 +225,16 @@ int launch_errors_from_draws(const int32_t* idx, const uint8_t* type, long long 
     return launch_check("errors_from_draws");
 }
 
-int launch_syndrome(const Code& c, const uint8_t* x, const uint8_t* z, long long B, uint8_t* sX, uint8_t* sZ,
-                    hipStream_t st)
+int launch_syndrome(const Code& c, const int32_t* chkVar, const uint8_t* x, const uint8_t* z, long long B,
+                    uint8_t* sX, uint8_t* sZ, hipStream_t st)
 {
     if (B <= 0) return QEC_OK;
+    if (chkVar != nullptr) {
+        const long long tot = B * (c.mX + c.mZ);
+        hipLaunchKernelGGL(syndrome_csr_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, x, z, chkVar, B,
+                           c.n, c.mX, c.mZ, c.L, sX, sZ);
+        return launch_check("syndrome_csr");
+    }
     if (!c.is_qc || c.J * c.L > 128 || c.K * c.L > 128) return fail(QEC_ERR_UNSUPPORTED, "syndrome kernel: needs a QC code");
     SynArgs a{};
     a.x = x; a.z = z; a.sX = sX; a.sZ = sZ; a.B = B;

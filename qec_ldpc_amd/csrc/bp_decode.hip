@@ -40,15 +40,41 @@
 
 namespace qec {
 
-// Compile-time design options (tools/kbench sweeps them; the defaults are the measured best):
+// Design options.  Each kernel variant carries its own measured choice of the first three
+// (Tune<> in the variant table below); defining one of those macros to 0 or 1 overrides it
+// for every variant.  The rest are global experiment switches.  tools/kbench sweeps them.
 //   QEC_RELABEL      spanning-tree lane relabelling (fewer ds_bpermute, but more distinct shifts)
 //   QEC_MASK_SELECT  rotation base chosen by a constant lane mask instead of hoisted addresses
 #ifndef QEC_RELABEL
-#define QEC_RELABEL 0
+#define QEC_RELABEL -1
 #endif
 #ifndef QEC_MASK_SELECT
 #define QEC_MASK_SELECT 0
 #endif
+//   QEC_PIPELINE     1: issue column l+1's gathers before column l's arithmetic; 2: and pin
+//                    that order with a scheduling barrier
+#ifndef QEC_PIPELINE
+#define QEC_PIPELINE 0
+#endif
+//   QEC_FASTDIV      guarded short division (see div_short below)
+#ifndef QEC_FASTDIV
+#define QEC_FASTDIV -1
+#endif
+//   QEC_ZEROSKIP     a column whose every numerator is +0 (and denominator > 0) on every live
+//                    lane gets q = +0 without dividing (IEEE: +0 / d = +0 for d > 0)
+#ifndef QEC_ZEROSKIP
+#define QEC_ZEROSKIP -1
+#endif
+#define QEC_PICK(macro, dflt) ((macro) >= 0 ? (macro) != 0 : (dflt))
+
+// Per-variant tuning: minimum waves per SIMD for the register allocator, and the options above.
+template <int MINW_, bool RELABEL_, bool ZEROSKIP_, bool FASTDIV_>
+struct Tune {
+    static constexpr int kMinWaves = MINW_;
+    static constexpr bool kRelabel = QEC_PICK(QEC_RELABEL, RELABEL_);
+    static constexpr bool kZeroSkip = QEC_PICK(QEC_ZEROSKIP, ZEROSKIP_);
+    static constexpr bool kFastDiv = QEC_PICK(QEC_FASTDIV, FASTDIV_);
+};
 
 constexpr int kMaxRL = 128;  // largest R*L a kernel argument block carries
 constexpr int kMaxR = 16;
@@ -79,9 +105,9 @@ struct BpArgs {
 // With C[l] = E[0][l] and D[r] = (C[0] - E[r][0]) mod P the R + L - 1 blocks of row 0 and
 // column 0 need no rotation at all (a spanning tree of the block graph), so those edges skip
 // the ds_bpermute in both directions.  Arithmetic (and so every output bit) is unchanged.
-inline void relabel(const int* E, int R, int L, int P, int* S, int* D, int* C)
+inline void relabel(const int* E, int R, int L, int P, bool on, int* S, int* D, int* C)
 {
-    if (!QEC_RELABEL) {
+    if (!on) {
         for (int k = 0; k < R * L; ++k) S[k] = E[k];
         for (int r = 0; r < R; ++r) D[r] = 0;
         for (int l = 0; l < L; ++l) C[l] = 0;
@@ -120,7 +146,7 @@ struct RuntimeShifts {
 // Compile-time: exponent tables produced by the QC_LDPC_CSS generator formula
 // (QEC_LDPC/QEC_LDPC_CSS.cu:37-90) evaluated by the compiler, so every rotation
 // address is a loop-invariant constant of the lane index.
-template <int J_, int K_, int L_, int P_, int S_, int T_>
+template <int J_, int K_, int L_, int P_, int S_, int T_, bool RL_>
 struct GeneratedShifts {
     static constexpr bool kStatic = true;
     static constexpr int kP = P_;
@@ -151,9 +177,9 @@ struct GeneratedShifts {
             for (int l = 0; l < L_; ++l)
                 t.EZ[k][l] = (int)(((((l < L_ / 2) ? (T_ * sp(l - k - 1)) % P_ : P_ - sp(k + l)) % P_) + P_) % P_);
         // relabel() on the 2-D tables (same rule, written out for constant evaluation)
-        for (int l = 0; l < L_; ++l) { t.CX[l] = QEC_RELABEL ? t.EX[0][l] : 0; t.CZ[l] = QEC_RELABEL ? t.EZ[0][l] : 0; }
-        for (int r = 0; r < J_; ++r) t.DX[r] = QEC_RELABEL ? ((t.CX[0] - t.EX[r][0]) % P_ + P_) % P_ : 0;
-        for (int r = 0; r < K_; ++r) t.DZ[r] = QEC_RELABEL ? ((t.CZ[0] - t.EZ[r][0]) % P_ + P_) % P_ : 0;
+        for (int l = 0; l < L_; ++l) { t.CX[l] = RL_ ? t.EX[0][l] : 0; t.CZ[l] = RL_ ? t.EZ[0][l] : 0; }
+        for (int r = 0; r < J_; ++r) t.DX[r] = RL_ ? ((t.CX[0] - t.EX[r][0]) % P_ + P_) % P_ : 0;
+        for (int r = 0; r < K_; ++r) t.DZ[r] = RL_ ? ((t.CZ[0] - t.EZ[r][0]) % P_ + P_) % P_ : 0;
         for (int r = 0; r < J_; ++r)
             for (int l = 0; l < L_; ++l) t.SX[r][l] = ((t.EX[r][l] + t.DX[r] - t.CX[l]) % P_ + P_) % P_;
         for (int r = 0; r < K_; ++r)
@@ -190,6 +216,7 @@ __device__ __forceinline__ int bperm_i(int addr, int v) { return __builtin_amdgc
 struct Lane {
     int i, gb;   // in-group index, group base lane
     int b0, b1;  // bpermute bases (laundered once per iteration so they stay cheap to reuse)
+    bool live;   // lane belongs to a syndrome of this batch
 };
 
 template <int P_>
@@ -241,6 +268,37 @@ __device__ __forceinline__ bool group_all(bool pred, int gb, int P)
 
 __device__ __forceinline__ bool outside(float x) { return !(x > 0.01f && x < 0.99f); }
 
+// ---- correctly rounded division, with a short path -----------------------------
+// hipcc lowers the IEEE fp32 quotient n / d to 11 instructions:
+//   D = div_scale(d), r = rcp(D), e = fma(-D, r, 1), r = fma(e, r, r), N = div_scale(n),
+//   q = N r, e = fma(-D, q, N), q = fma(e, r, q), e = fma(-D, q, N), q = div_fmas(e, r, q),
+//   q = div_fixup(q, d, n).
+// div_scale only rescales (by 2^64) when an operand or the quotient is near the ends of
+// the exponent range, and div_fixup only changes special cases (0, inf, NaN, over/underflow);
+// with d in [2^-98, 2], n = +0 or n in [2^-98, d] neither fires (no scaling, VCC = 0, so
+// div_fmas is a plain fma, and every residual fma is exact), so the same arithmetic without
+// them gives the same bits (8 instructions, measured 14.4 vs 24.7 SIMD-cycles).  The guard
+// below is evaluated for a whole column of divisions and the short path taken only when every
+// live lane of the wave passes it; otherwise the full sequence runs.
+__device__ __forceinline__ float div_short(float n, float d)
+{
+    float r = __builtin_amdgcn_rcpf(d);
+    const float e = __builtin_fmaf(-d, r, 1.0f);
+    r = __builtin_fmaf(e, r, r);
+    float q = n * r;
+    const float e2 = __builtin_fmaf(-d, q, n);
+    q = __builtin_fmaf(e2, r, q);
+    const float e3 = __builtin_fmaf(-d, q, n);
+    return __builtin_fmaf(e3, r, q);
+}
+// n = t1 >= 0 and d = t0 + t1 with t0, t1 products of probabilities in [0, 1] (so d <= 2):
+// short path valid iff d >= 2^-98 (a float compare: NaN fails) and n is +0 or >= 2^-98
+// (bit patterns of non-negative floats order like unsigned integers; +0 - 1 wraps to the top).
+__device__ __forceinline__ bool div_short_ok(float n, float d)
+{
+    return (d >= 0x1p-98f) & ((__float_as_uint(n) - 1u) >= (__float_as_uint(0x1p-98f) - 1u));
+}
+
 // ---- one sector (X: R = J, Z: R = K) ------------------------------------
 // EqNodeUpdate (DecoderCPU.h:150-186) for checks (r, i), r = 0..R-1: lane-local.
 template <int R, int L>
@@ -279,29 +337,50 @@ __device__ __forceinline__ void check_pass(float (&msg)[R][L], uint32_t sbits)
 // check messages by forward rotation, update, scatter back by the inverse rotation.
 // LAST: the final iteration includes the self message (DecoderCPU.h:216).
 // Returns the hard-decision mask (bit l) of the new messages when HD is set.
-template <int R, int L, int SEC, bool LAST, bool HD, class SH>
+template <int R, int L, int SEC, bool LAST, bool HD, class SH, class TU>
 __device__ __forceinline__ uint32_t var_pass(const BpArgs& a, float (&msg)[R][L], const Lane& ln, float pp,
                                              float one_minus_pp)
 {
+    // the short division's guard assumes every message is a probability in [0, 1], which
+    // holds by induction when p' is (DecoderCPU.h:135-229); other p' always take the full path
+    const bool pp_ok = pp >= 0.0f && pp <= 1.0f;
     const int P = SH::P(a);
     const int* et = SH::template table<SEC>(a);
     uint32_t hdmask = 0;
+    // QEC_PIPELINE: the gathers of column l + 1 are issued before column l is computed, so
+    // their ds_bpermute latency hides behind column l's arithmetic in the same wave.
+    float gnext[R];
+    if constexpr (QEC_PIPELINE) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) gnext[r] = rot<SH>(msg[r][0], ln, SH::template shift<SEC, L>(et, r, 0));
+    }
 #pragma unroll
     for (int l = 0; l < L; ++l) {
         float gv[R], bv[R], qv[R];
+        if constexpr (QEC_PIPELINE) {
 #pragma unroll
-        for (int r = 0; r < R; ++r) {
-            const int sh = SH::template shift<SEC, L>(et, r, l);
-            gv[r] = rot<SH>(msg[r][l], ln, sh);
-            bv[r] = 1.0f - gv[r];
+            for (int r = 0; r < R; ++r) gv[r] = gnext[r];
+            if (l + 1 < L) {
+#pragma unroll
+                for (int r = 0; r < R; ++r)
+                    gnext[r] = rot<SH>(msg[r][l + 1], ln, SH::template shift<SEC, L>(et, r, l + 1));
+            }
+            if constexpr (QEC_PIPELINE >= 2) __builtin_amdgcn_sched_barrier(0);
+        } else {
+#pragma unroll
+            for (int r = 0; r < R; ++r) gv[r] = rot<SH>(msg[r][l], ln, SH::template shift<SEC, L>(et, r, l));
         }
+#pragma unroll
+        for (int r = 0; r < R; ++r) bv[r] = 1.0f - gv[r];
+        // numerators / denominators of the R outgoing messages (LAST: one, shared)
+        constexpr int ND = LAST ? 1 : R;
+        float num[ND], den[ND];
         if constexpr (LAST) {
             float P0 = one_minus_pp, P1 = pp;
 #pragma unroll
             for (int k = 0; k < R; ++k) { P0 = P0 * bv[k]; P1 = P1 * gv[k]; }
-            const float q = P1 / (P0 + P1);
-#pragma unroll
-            for (int r = 0; r < R; ++r) qv[r] = q;
+            num[0] = P1;
+            den[0] = P0 + P1;
         } else {
             float pre0 = one_minus_pp, pre1 = pp;
 #pragma unroll
@@ -309,10 +388,43 @@ __device__ __forceinline__ uint32_t var_pass(const BpArgs& a, float (&msg)[R][L]
                 float t0 = pre0, t1 = pre1;
 #pragma unroll
                 for (int k = j + 1; k < R; ++k) { t0 = t0 * bv[k]; t1 = t1 * gv[k]; }
-                qv[j] = t1 / (t0 + t1);
+                num[j] = t1;
+                den[j] = t0 + t1;
                 if (j + 1 < R) { pre0 = pre0 * bv[j]; pre1 = pre1 * gv[j]; }
             }
         }
+        float qd[ND];
+        bool zero = false, fast = false;
+        if constexpr (TU::kZeroSkip) {
+            uint32_t nb = 0;
+            bool dpos = true;
+#pragma unroll
+            for (int j = 0; j < ND; ++j) {
+                nb |= __float_as_uint(num[j]);
+                dpos &= den[j] > 0.0f;
+            }
+            zero = __all((nb == 0u && dpos) | !ln.live);
+        }
+        if constexpr (TU::kFastDiv) {
+            if (!zero) {
+                bool ok = true;
+#pragma unroll
+                for (int j = 0; j < ND; ++j) ok &= div_short_ok(num[j], den[j]);
+                fast = pp_ok && __all(ok | !ln.live);
+            }
+        }
+        if (zero) {
+#pragma unroll
+            for (int j = 0; j < ND; ++j) qd[j] = 0.0f;
+        } else if (fast) {
+#pragma unroll
+            for (int j = 0; j < ND; ++j) qd[j] = div_short(num[j], den[j]);
+        } else {
+#pragma unroll
+            for (int j = 0; j < ND; ++j) qd[j] = num[j] / den[j];
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r) qv[r] = qd[LAST ? 0 : r];
         if constexpr (HD) {
             bool hd = false;
 #pragma unroll
@@ -362,7 +474,7 @@ __device__ __forceinline__ bool lane_syndrome_ok(const BpArgs& a, uint32_t hdmas
 }
 
 // One BP iteration; returns true if this group stops after it.
-template <int R, int L, int SEC, int STOP, bool LAST, class SH>
+template <int R, int L, int SEC, int STOP, bool LAST, class SH, class TU>
 __device__ __forceinline__ bool iteration(const BpArgs& a, float (&msg)[R][L], uint32_t sbits, int n, Lane& ln,
                                           float pp, float one_minus_pp)
 {
@@ -371,7 +483,7 @@ __device__ __forceinline__ bool iteration(const BpArgs& a, float (&msg)[R][L], u
     // loop instead of being hoisted into ~2 R L live registers
     if constexpr (QEC_MASK_SELECT) asm volatile("" : "+v"(ln.b0), "+v"(ln.b1));
     check_pass<R, L>(msg, sbits);
-    const uint32_t hdmask = var_pass<R, L, SEC, LAST, STOP == QEC_STOP_SYNDROME, SH>(a, msg, ln, pp, one_minus_pp);
+    const uint32_t hdmask = var_pass<R, L, SEC, LAST, STOP == QEC_STOP_SYNDROME, SH, TU>(a, msg, ln, pp, one_minus_pp);
     if constexpr (STOP == QEC_STOP_REF) {
         if (n % 10 == 0) return group_all(lane_converged<R, L>(msg), ln.gb, P);  // DecoderCPU.h:287-290
     } else if constexpr (STOP == QEC_STOP_SYNDROME) {
@@ -380,7 +492,7 @@ __device__ __forceinline__ bool iteration(const BpArgs& a, float (&msg)[R][L], u
     return false;
 }
 
-template <int R, int L, int SEC, int STOP, class SH>
+template <int R, int L, int SEC, int STOP, class SH, class TU>
 __device__ __forceinline__ void decode_sector(const BpArgs& a, Lane& ln, long long b, bool in_range, float pp,
                                               uint32_t& flags, int& iters_out)
 {
@@ -416,12 +528,12 @@ __device__ __forceinline__ void decode_sector(const BpArgs& a, Lane& ln, long lo
         }
         if (active) {
             ++it;
-            if (iteration<R, L, SEC, STOP, false, SH>(a, msg, sbits, n, ln, pp, one_minus_pp)) active = false;
+            if (iteration<R, L, SEC, STOP, false, SH, TU>(a, msg, sbits, n, ln, pp, one_minus_pp)) active = false;
         }
     }
     if (n == N - 1 && active) {
         ++it;
-        iteration<R, L, SEC, STOP, true, SH>(a, msg, sbits, n, ln, pp, one_minus_pp);
+        iteration<R, L, SEC, STOP, true, SH, TU>(a, msg, sbits, n, ln, pp, one_minus_pp);
     }
 
     // ---- post-processing of Decode (DecoderCPU.h:354-384) ----
@@ -466,8 +578,8 @@ __device__ __forceinline__ void decode_sector(const BpArgs& a, Lane& ln, long lo
 
 // MINW: minimum waves per SIMD the register allocator must allow (5 -> <= 96 VGPRs), measured
 // per variant with tools/kbench (P61: 5 waves beat 4 by 4 %; see profiles/).
-template <int RX, int RZ, int L, int STOP, class SH, int MINW>
-__global__ __launch_bounds__(64 * QEC_WAVES_PER_BLOCK, (QEC_MIN_WAVES_PER_EU ? QEC_MIN_WAVES_PER_EU : MINW))
+template <int RX, int RZ, int L, int STOP, class SH, class TU>
+__global__ __launch_bounds__(64 * QEC_WAVES_PER_BLOCK, (QEC_MIN_WAVES_PER_EU ? QEC_MIN_WAVES_PER_EU : TU::kMinWaves))
 void bp_decode_kernel(const BpArgs a)
 {
     const int lane = threadIdx.x & 63;
@@ -485,9 +597,9 @@ void bp_decode_kernel(const BpArgs a)
     const float pp = 2.0f / 3.0f * a.errorProbability;
     uint32_t flags = 0;
     int itX = 0, itZ = 0;
-    Lane ln{i, gb, 4 * (gb + i), 4 * (gb + i + P)};
-    decode_sector<RX, L, 0, STOP, SH>(a, ln, b, in_range, pp, flags, itX);
-    decode_sector<RZ, L, 1, STOP, SH>(a, ln, b, in_range, pp, flags, itZ);
+    Lane ln{i, gb, 4 * (gb + i), 4 * (gb + i + P), in_range};
+    decode_sector<RX, L, 0, STOP, SH, TU>(a, ln, b, in_range, pp, flags, itX);
+    decode_sector<RZ, L, 1, STOP, SH, TU>(a, ln, b, in_range, pp, flags, itZ);
     if (in_range && i == 0) {
         a.flags[b] = (uint8_t)flags;
         if (a.iters != nullptr) {
@@ -503,43 +615,49 @@ using KernelFn = void (*)(const BpArgs);
 struct Variant {
     int J, K, L;
     int P, sigma, tau;  // P > 0: specialised to the generator's tables for these parameters
+    bool relabel;       // runtime-shift variants: relabel the lane tables at launch
     KernelFn fn[3];     // indexed by stop rule
     const char* name;
 };
 
-template <int J, int K, int L, class SH, int MINW>
+template <int J, int K, int L, class SH, class TU>
 static Variant make_variant(int P, int S, int T, const char* name)
 {
-    return Variant{J, K, L, P, S, T,
-                   {bp_decode_kernel<J, K, L, QEC_STOP_REF, SH, MINW>, bp_decode_kernel<J, K, L, QEC_STOP_FIXED, SH, MINW>,
-                    bp_decode_kernel<J, K, L, QEC_STOP_SYNDROME, SH, MINW>},
+    return Variant{J, K, L, P, S, T, TU::kRelabel,
+                   {bp_decode_kernel<J, K, L, QEC_STOP_REF, SH, TU>, bp_decode_kernel<J, K, L, QEC_STOP_FIXED, SH, TU>,
+                    bp_decode_kernel<J, K, L, QEC_STOP_SYNDROME, SH, TU>},
                    name};
 }
-template <int J, int K, int L, int MINW = 1>
+// Tune<min waves per SIMD, relabel, zero-skip, short division>
+template <int J, int K, int L, class TU = Tune<1, false, true, true>>
 static Variant rt()
 {
-    return make_variant<J, K, L, RuntimeShifts, MINW>(0, 0, 0, "wave-circulant runtime-shift");
+    return make_variant<J, K, L, RuntimeShifts, TU>(0, 0, 0, "wave-circulant runtime-shift");
 }
-template <int J, int K, int L, int P, int S, int T, int MINW>
+template <int J, int K, int L, int P, int S, int T, class TU>
 static Variant gen()
 {
-    return make_variant<J, K, L, GeneratedShifts<J, K, L, P, S, T>, MINW>(P, S, T, "wave-circulant generated-shift");
+    return make_variant<J, K, L, GeneratedShifts<J, K, L, P, S, T, TU::kRelabel>, TU>(P, S, T,
+                                                                                      "wave-circulant generated-shift");
 }
 
+// Measured per variant with tools/kbench (profiles/r01/): P61 4 waves + relabel + zero-skip +
+// short division 7.11 ms vs 9.46 ms without them; P7 (9 syndromes per wave, so whole-wave
+// zero columns are rare) keeps 8 waves and only the short division.
 static const Variant kVariants[] = {
     // specialised: the two code files the reference ships
-    gen<4, 5, 10, 61, 9, 49, 5>(),
-    gen<3, 3, 6, 7, 2, 3, 8>(),
+    gen<4, 5, 10, 61, 9, 49, Tune<4, true, true, true>>(),
+    gen<3, 3, 6, 7, 2, 3, Tune<8, false, false, true>>(),
 #ifndef QEC_KBENCH_MINIMAL  // experiment builds (tools/kbench) only compile the shipped-code kernels
     // runtime shifts, any P <= 64 with these block shapes
     rt<4, 5, 10>(),
-    rt<3, 3, 6, 6>(),
-    rt<2, 3, 6, 6>(),
+    rt<3, 3, 6, Tune<6, false, false, true>>(),
+    rt<2, 3, 6, Tune<6, false, false, true>>(),
     rt<3, 4, 8>(),
     rt<4, 4, 8>(),
     rt<3, 5, 10>(),
     rt<4, 6, 12>(),
-    rt<2, 2, 4, 8>(),
+    rt<2, 2, 4, Tune<8, false, false, true>>(),
 #endif
 };
 
@@ -582,8 +700,8 @@ int launch_decode(const void* variant, const Code& c, const uint8_t* sX, const u
     a.errorProbability = errorProbability;
     a.maxIter = maxIter < 0 ? 0 : maxIter;
     a.stop = stop;
-    relabel(c.EX.data(), c.J, c.L, c.P, a.SX, a.DX, a.CX);
-    relabel(c.EZ.data(), c.K, c.L, c.P, a.SZ, a.DZ, a.CZ);
+    relabel(c.EX.data(), c.J, c.L, c.P, v->relabel, a.SX, a.DX, a.CX);
+    relabel(c.EZ.data(), c.K, c.L, c.P, v->relabel, a.SZ, a.DZ, a.CZ);
     const int wavesPerBlock = QEC_WAVES_PER_BLOCK;
     const long long waves = (B + a.G - 1) / a.G;
     const long long blocks = (waves + wavesPerBlock - 1) / wavesPerBlock;

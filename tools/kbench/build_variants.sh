@@ -1,25 +1,39 @@
 #!/bin/bash
 # Build experimental variants of libqecldpc.so into build/variants/<name>/ (same sources,
-# different compile flags / macros).  Used by tools/kbench/compare.py on the GPU box.
+# different compile flags / macros for bp_decode.hip; the other objects are shared).
+# Used by tools/kbench/compare.py on the GPU box.
+#   tools/kbench/build_variants.sh name[:flags] ...     e.g.  cur  pipe:-DQEC_PIPELINE=1
 set -e
 cd "$(dirname "$0")/../.."
 HIPCC=/opt/rocm/bin/hipcc
 BASE="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -fno-slp-vectorize -w"
+COMMON=build/variants/_common
+mkdir -p $COMMON
+common() {
+  src=$1; obj=$COMMON/$(basename ${src%.*}).o; shift
+  if [ ! -f $obj ] || [ $src -nt $obj ]; then $HIPCC $BASE "$@" -c $src -o $obj; fi
+}
+common qec_ldpc_amd/csrc/code_model.cpp -x c++ &
+common qec_ldpc_amd/csrc/montecarlo.hip &
+common qec_ldpc_amd/csrc/capi.cpp -x hip &
+common qec_ldpc_amd/csrc/bp_sparse.hip &
+wait
 build() {
   name=$1; shift
   out=build/variants/$name
   mkdir -p $out
-  $HIPCC $BASE "$@" -c qec_ldpc_amd/csrc/bp_decode.hip -o $out/bp_decode.o &
-  $HIPCC $BASE -x c++ -c qec_ldpc_amd/csrc/code_model.cpp -o $out/code_model.o &
-  $HIPCC $BASE -c qec_ldpc_amd/csrc/montecarlo.hip -o $out/montecarlo.o &
-  $HIPCC $BASE -x hip -c qec_ldpc_amd/csrc/capi.cpp -o $out/capi.o &
-  wait
-  $HIPCC --offload-arch=gfx950 -shared -fPIC -o $out/libqecldpc.so $out/*.o
+  $HIPCC $BASE -DQEC_KBENCH_MINIMAL "$@" -c qec_ldpc_amd/csrc/bp_decode.hip -o $out/bp_decode.o
+  $HIPCC --offload-arch=gfx950 -shared -fPIC -o $out/libqecldpc.so $out/bp_decode.o $COMMON/*.o
   echo "built $name"
 }
+pids=()
 while [ $# -gt 0 ]; do
   spec=$1; shift
   name=${spec%%:*}; flags=${spec#*:}
   [ "$flags" = "$spec" ] && flags=""
-  build $name $flags
+  flags=${flags//,/ }
+  build $name $flags &
+  pids+=($!)
+  if [ ${#pids[@]} -ge 6 ]; then wait ${pids[0]}; pids=("${pids[@]:1}"); fi
 done
+wait

@@ -13,7 +13,12 @@ Prints one JSON line (rank 0).  Extra objects:
                    schedule) over its HIP-event-timed launch duration, vs 8 TB/s;
                    the engine keeps messages in VGPRs, so frac > 1 means it moves
                    less than that schedule's bytes.
-  valu          -- the same launch against the fp32 VALU issue ceiling.
+  full_arithmetic -- the same batch re-timed with QEC_OPT_HARD_PATHS off (every
+                   iteration in full fp32 arithmetic, no hard-message forms), with a
+                   bit-identity check against the timed run's outputs.
+  valu          -- analytical full-arithmetic VALU lane-ops per launch over the
+                   full_arithmetic launch time, vs the fp32 VALU issue ceiling (on the
+                   hard-path launch the analytical count would over-count the work).
   cpu_baseline  -- oracle (CPU restatement of DecoderCPU, OpenMP) on host cores,
                    rank 0 at N = 1 only, bounded sample of the same workload.
 """
@@ -76,6 +81,9 @@ def main():
     ap.add_argument("--stop", choices=["fixed", "ref", "syndrome"], default="fixed")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--hard-paths", type=int, default=1, help="QEC_OPT_HARD_PATHS for the timed run")
+    ap.add_argument("--no-full-arith", action="store_true",
+                    help="skip the full_arithmetic re-timing (profiling runs: keeps the launch average clean)")
     args = ap.parse_args()
 
     import torch
@@ -97,6 +105,7 @@ def main():
     iters = args.iters if args.iters is not None else it_def
     code = q.Quantum_LDPC_Code.createFromFile(code_path(fname))
     dec = q.DecoderGPU(code, local)
+    dec.set_option("hard_paths", args.hard_paths)
     B = args.batch
 
     # rank's shard of the sample index space, [rank*B, (rank+1)*B), drawn on the device
@@ -153,7 +162,11 @@ def main():
     bytes_per_syn = 16 * (EX * it_mean[0] + EZ * it_mean[1]) + io
     achieved_gbs = bytes_per_syn * B / (kernel_ms * 1e-3) / 1e9
     ops = lane_ops_per_syndrome(code, 1) * (it_mean[0] + it_mean[1]) / 2.0
-    achieved_tops = ops * B / (kernel_ms * 1e-3) / 1e12
+    full = None
+    if args.hard_paths and not args.no_full_arith:
+        full = full_arithmetic(dec, step, stream, B, (eX, eZ, fl, its))
+    valu_ms = full["kernel_ms"] if full else kernel_ms
+    achieved_tops = ops * B / (valu_ms * 1e-3) / 1e12
     traffic = None
     prof = os.path.join(ROOT, "profiles", "pmc_%s.json" % args.code)
     if os.path.exists(prof):
@@ -187,8 +200,11 @@ def main():
                      "frac": round(achieved_gbs / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "algorithmic_bytes_per_launch": int(bytes_per_syn * B), "kernel_ms": round(kernel_ms, 4)},
         "valu": {"achieved": round(achieved_tops, 2), "peak": VALU_PEAK_TOPS, "unit": "Tlane-op/s",
-                 "frac": round(achieved_tops / VALU_PEAK_TOPS, 4)},
+                 "frac": round(achieved_tops / VALU_PEAK_TOPS, 4), "kernel_ms": round(valu_ms, 4),
+                 "launch": "full_arithmetic" if full else "timed"},
     }
+    if full:
+        out["full_arithmetic"] = full
     if args.stop != "fixed":
         hist = np.bincount(it_np.ravel(), minlength=iters + 1)
         out["iteration_histogram"] = {str(k): int(v) for k, v in enumerate(hist) if v}
@@ -200,6 +216,28 @@ def main():
         dist.destroy_process_group()
     if rank == 0:
         print(json.dumps(out), flush=True)
+
+
+def full_arithmetic(dec, step, stream, B, outs, reps=3):
+    """Re-time the step with the hard-message paths off and check the outputs are the same bits."""
+    import torch
+    ref = [t.clone() for t in outs]
+    dec.set_option("hard_paths", 0)
+    try:
+        step()
+        ms = []
+        for _ in range(reps):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(stream)
+            step()
+            b.record(stream)
+            torch.cuda.synchronize()
+            ms.append(a.elapsed_time(b))
+    finally:
+        dec.set_option("hard_paths", 1)
+    same = all(torch.equal(r, t) for r, t in zip(ref, outs))
+    k = float(np.median(ms))
+    return {"kernel_ms": round(k, 4), "syndromes_per_s": round(B / k * 1e3, 1), "identical": bool(same)}
 
 
 def cpu_baseline(code, fname, sX_h, sZ_h, p, iters, args, eX, eZ, fl):

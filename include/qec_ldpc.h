@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define QEC_LDPC_ABI_VERSION 2
+#define QEC_LDPC_ABI_VERSION 3
 
 /* status codes */
 enum {
@@ -122,6 +122,14 @@ qec_decoder* qec_decoder_create(const qec_code* code, int device, size_t max_bat
  * J / K, DecoderCPU.h:41-84). */
 qec_decoder* qec_decoder_create_engine(const qec_code* code, int device, size_t max_batch, int engine);
 int qec_decoder_destroy(qec_decoder* dec);
+/* Decoder options (no reference analogue: DecoderCPU has none).
+ *   QEC_OPT_HARD_PATHS (default 1): once every message of a sector is exactly +0 or 1.0 the
+ *     wave-circulant kernels switch to the exact hard-message forms of the check and variable
+ *     updates (bp_decode.hip, check_pass_hard / var_pass).  Outputs are bit-identical either
+ *     way; 0 forces the full arithmetic every iteration (for measurement). */
+enum { QEC_OPT_HARD_PATHS = 1 };
+int qec_decoder_set_option(qec_decoder* dec, int option, int value);
+int qec_decoder_get_option(const qec_decoder* dec, int option, int* value);
 /* which kernel variant serves this code: writes a short name (e.g. "wave-circulant P=61 G=1") */
 int qec_decoder_describe(const qec_decoder* dec, char* buf, size_t len);
 

@@ -26,6 +26,7 @@ CONVERGENCE_FAIL_X = 4
 CONVERGENCE_FAIL_Z = 8
 STOP = {"ref": 0, "fixed": 1, "syndrome": 2}
 ENGINE = {"auto": 0, "circulant": 1, "sparse": 2}
+OPTION = {"hard_paths": 1}
 
 # every symbol include/qec_ldpc.h declares
 EXPORTS = (
@@ -33,6 +34,7 @@ EXPORTS = (
     "qec_code_load", "qec_code_generate", "qec_code_free", "qec_code_params", "qec_code_exponents",
     "qec_code_pcm", "qec_code_describe", "qec_code_syndrome", "qec_code_check_logical",
     "qec_decoder_create", "qec_decoder_create_engine", "qec_decoder_destroy", "qec_decoder_describe",
+    "qec_decoder_set_option", "qec_decoder_get_option",
     "qec_decode_batch", "qec_decode_batch_dev",
     "qec_sample_fixed_weight", "qec_get_statistics",
     "qec_sample_depolarizing_dev", "qec_syndrome_dev", "qec_statistics_dev", "qec_monte_carlo",
@@ -95,6 +97,8 @@ def lib():
             "qec_decoder_create_engine": (vp, [vp, i, sz, i]),
             "qec_decoder_destroy": (i, [vp]),
             "qec_decoder_describe": (i, [vp, ctypes.c_char_p, sz]),
+            "qec_decoder_set_option": (i, [vp, i, i]),
+            "qec_decoder_get_option": (i, [vp, i, vp]),
             "qec_decode_batch": (i, [vp, vp, vp, sz, f, i, i, vp, vp, vp, vp, vp]),
             "qec_decode_batch_dev": (i, [vp, vp, vp, sz, f, i, i, vp, vp, vp, vp, vp, vp]),
             "qec_sample_fixed_weight": (i, [ctypes.c_uint32, i, sz, i, vp, vp]),
@@ -261,6 +265,15 @@ class DecoderGPU:
         buf = ctypes.create_string_buffer(256)
         _check(lib().qec_decoder_describe(self._h, buf, 256), "qec_decoder_describe")
         return buf.value.decode()
+
+    def set_option(self, name, value):
+        """qec_decoder_set_option (include/qec_ldpc.h): e.g. set_option("hard_paths", 0)."""
+        _check(lib().qec_decoder_set_option(self._h, OPTION[name], int(value)), "qec_decoder_set_option")
+
+    def get_option(self, name):
+        v = ctypes.c_int(0)
+        _check(lib().qec_decoder_get_option(self._h, OPTION[name], ctypes.byref(v)), "qec_decoder_get_option")
+        return v.value
 
     def decode_batch(self, sX, sZ, p, max_iter, stop="ref", want_iters=False, want_q=False):
         """Host-buffer batch decode -> (eX, eZ, flags, iters|None, q|None)."""

@@ -65,16 +65,30 @@ namespace qec {
 #ifndef QEC_ZEROSKIP
 #define QEC_ZEROSKIP -1
 #endif
+//   QEC_SATURATE     hard-message fast paths once every message of a sector is exactly 0 or 1
+//                    (see check_pass_hard / var_pass below)
+#ifndef QEC_SATURATE
+#define QEC_SATURATE -1
+#endif
 #define QEC_PICK(macro, dflt) ((macro) >= 0 ? (macro) != 0 : (dflt))
 
 // Per-variant tuning: minimum waves per SIMD for the register allocator, and the options above.
-template <int MINW_, bool RELABEL_, bool ZEROSKIP_, bool FASTDIV_>
+template <int MINW_, bool RELABEL_, bool ZEROSKIP_, bool FASTDIV_, bool SATURATE_ = false>
 struct Tune {
     static constexpr int kMinWaves = MINW_;
     static constexpr bool kRelabel = QEC_PICK(QEC_RELABEL, RELABEL_);
     static constexpr bool kZeroSkip = QEC_PICK(QEC_ZEROSKIP, ZEROSKIP_);
     static constexpr bool kFastDiv = QEC_PICK(QEC_FASTDIV, FASTDIV_);
+    static constexpr bool kSaturate = QEC_PICK(QEC_SATURATE, SATURATE_);
 };
+
+// true iff pred holds on every live lane of the wave (lanes outside the batch, or masked off
+// by a finished group, do not vote)
+__device__ __forceinline__ bool all_live(bool pred, bool live) { return __ballot(live && !pred) == 0ull; }
+
+// The hard-message paths need 0 < p' < 1: then every message lies in [0, 1], zeros are +0,
+// and q - q*q == 0 exactly iff q is +0 or 1 (NaN fails the test).
+__device__ __forceinline__ bool hard_ok(float pp) { return pp > 0.0f && pp < 1.0f; }
 
 constexpr int kMaxRL = 128;  // largest R*L a kernel argument block carries
 constexpr int kMaxR = 16;
@@ -92,6 +106,7 @@ struct BpArgs {
     int P, G, n, mX, mZ;
     float errorProbability;
     int maxIter, stop;
+    int hardPaths;  // 0 disables the hard-message paths of variants compiled with them (QEC_OPT_HARD_PATHS)
     // lane-relabelled circulant tables (see relabel() below)
     int SX[kMaxRL], SZ[kMaxRL];  // rotation of block (r, l) between check and variable views
     int DX[kMaxR], DZ[kMaxR];    // check-view lane lambda holds check (r, (lambda + D[r]) mod P)
@@ -333,14 +348,36 @@ __device__ __forceinline__ void check_pass(float (&msg)[R][L], uint32_t sbits)
     }
 }
 
+// EqNodeUpdate when every incoming message is exactly +0 or 1.0 (a "hard" sector): then every
+// factor 1 - 2q is exactly +1 or -1, every leave-one-out product is exactly (-1)^(ones among
+// the others), and 0.5 * (1 -/+ t) is exactly +0 or 1.0 -- i.e. the output is the parity
+// s XOR (ones among the others), which on the bit patterns {0, 0x3F800000} is an XOR.
+// Bit-identical to check_pass on such inputs.
+template <int R, int L>
+__device__ __forceinline__ void check_pass_hard(float (&msg)[R][L], uint32_t sbits)
+{
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        uint32_t x = ((sbits >> r) & 1u) ? 0x3F800000u : 0u;
+#pragma unroll
+        for (int l = 0; l < L; ++l) x ^= __float_as_uint(msg[r][l]);
+#pragma unroll
+        for (int l = 0; l < L; ++l) msg[r][l] = __uint_as_float(x ^ __float_as_uint(msg[r][l]));
+    }
+}
+
 // VarNodeUpdate (DecoderCPU.h:188-229) for variables (l, i): gather the R incoming
 // check messages by forward rotation, update, scatter back by the inverse rotation.
 // LAST: the final iteration includes the self message (DecoderCPU.h:216).
 // Returns the hard-decision mask (bit l) of the new messages when HD is set.
+// hard: in = every incoming (check->variable) message is exactly +0 or 1.0; out = so is every
+// outgoing one (only tracked when the hard-message paths are enabled for this launch).
 template <int R, int L, int SEC, bool LAST, bool HD, class SH, class TU>
 __device__ __forceinline__ uint32_t var_pass(const BpArgs& a, float (&msg)[R][L], const Lane& ln, float pp,
-                                             float one_minus_pp)
+                                             float one_minus_pp, bool& hard)
 {
+    const bool hard_in = hard;
+    uint32_t soft_bits = 0;  // OR of bits(q - q*q) over outputs not known to be hard: 0 iff all are 0 or 1
     // the short division's guard assumes every message is a probability in [0, 1], which
     // holds by induction when p' is (DecoderCPU.h:135-229); other p' always take the full path
     const bool pp_ok = pp >= 0.0f && pp <= 1.0f;
@@ -370,6 +407,24 @@ __device__ __forceinline__ uint32_t var_pass(const BpArgs& a, float (&msg)[R][L]
 #pragma unroll
             for (int r = 0; r < R; ++r) gv[r] = rot<SH>(msg[r][l], ln, SH::template shift<SEC, L>(et, r, l));
         }
+        // hard inputs: q_j = P1 / (P0 + P1) with every factor 0 or 1 is exactly the common value
+        // when all R inputs agree (all 1: p'/p' = 1; all 0: +0/(1-p') = +0); columns where some
+        // variable's inputs disagree (0/0 = NaN) take the arithmetic path below
+        bool done = false;
+        if constexpr (TU::kSaturate) {
+            if (hard_in && (LAST || R >= 2)) {
+                const uint32_t x0 = __float_as_uint(gv[0]);
+                bool same = true;
+#pragma unroll
+                for (int r = 1; r < R; ++r) same &= __float_as_uint(gv[r]) == x0;
+                if (all_live(same, ln.live)) {
+#pragma unroll
+                    for (int r = 0; r < R; ++r) qv[r] = gv[0];
+                    done = true;
+                }
+            }
+        }
+        if (!done) {
 #pragma unroll
         for (int r = 0; r < R; ++r) bv[r] = 1.0f - gv[r];
         // numerators / denominators of the R outgoing messages (LAST: one, shared)
@@ -403,14 +458,14 @@ __device__ __forceinline__ uint32_t var_pass(const BpArgs& a, float (&msg)[R][L]
                 nb |= __float_as_uint(num[j]);
                 dpos &= den[j] > 0.0f;
             }
-            zero = __all((nb == 0u && dpos) | !ln.live);
+            zero = all_live(nb == 0u && dpos, ln.live);
         }
         if constexpr (TU::kFastDiv) {
             if (!zero) {
                 bool ok = true;
 #pragma unroll
                 for (int j = 0; j < ND; ++j) ok &= div_short_ok(num[j], den[j]);
-                fast = pp_ok && __all(ok | !ln.live);
+                fast = pp_ok && all_live(ok, ln.live);
             }
         }
         if (zero) {
@@ -423,8 +478,15 @@ __device__ __forceinline__ uint32_t var_pass(const BpArgs& a, float (&msg)[R][L]
 #pragma unroll
             for (int j = 0; j < ND; ++j) qd[j] = num[j] / den[j];
         }
+        if constexpr (TU::kSaturate) {
+            if (!zero) {
+#pragma unroll
+                for (int j = 0; j < ND; ++j) soft_bits |= __float_as_uint(__builtin_fmaf(-qd[j], qd[j], qd[j]));
+            }
+        }
 #pragma unroll
         for (int r = 0; r < R; ++r) qv[r] = qd[LAST ? 0 : r];
+        }  // !done
         if constexpr (HD) {
             bool hd = false;
 #pragma unroll
@@ -437,6 +499,7 @@ __device__ __forceinline__ uint32_t var_pass(const BpArgs& a, float (&msg)[R][L]
             msg[r][l] = rot<SH>(qv[r], ln, sh == 0 ? 0 : P - sh);
         }
     }
+    if constexpr (TU::kSaturate) hard = a.hardPaths != 0 && hard_ok(pp) && all_live(soft_bits == 0u, ln.live);
     return hdmask;
 }
 
@@ -474,16 +537,21 @@ __device__ __forceinline__ bool lane_syndrome_ok(const BpArgs& a, uint32_t hdmas
 }
 
 // One BP iteration; returns true if this group stops after it.
+// hard: every variable->check message of this sector is exactly +0 or 1.0 (wave-uniform).
 template <int R, int L, int SEC, int STOP, bool LAST, class SH, class TU>
 __device__ __forceinline__ bool iteration(const BpArgs& a, float (&msg)[R][L], uint32_t sbits, int n, Lane& ln,
-                                          float pp, float one_minus_pp)
+                                          float pp, float one_minus_pp, bool& hard)
 {
     const int P = SH::P(a);
     // launder the permute bases so their per-rotation selects are recomputed inside the
     // loop instead of being hoisted into ~2 R L live registers
     if constexpr (QEC_MASK_SELECT) asm volatile("" : "+v"(ln.b0), "+v"(ln.b1));
-    check_pass<R, L>(msg, sbits);
-    const uint32_t hdmask = var_pass<R, L, SEC, LAST, STOP == QEC_STOP_SYNDROME, SH, TU>(a, msg, ln, pp, one_minus_pp);
+    if (TU::kSaturate && hard)
+        check_pass_hard<R, L>(msg, sbits);  // outputs are hard too: hard stays set for the var pass
+    else
+        check_pass<R, L>(msg, sbits);
+    const uint32_t hdmask =
+        var_pass<R, L, SEC, LAST, STOP == QEC_STOP_SYNDROME, SH, TU>(a, msg, ln, pp, one_minus_pp, hard);
     if constexpr (STOP == QEC_STOP_REF) {
         if (n % 10 == 0) return group_all(lane_converged<R, L>(msg), ln.gb, P);  // DecoderCPU.h:287-290
     } else if constexpr (STOP == QEC_STOP_SYNDROME) {
@@ -517,6 +585,7 @@ __device__ __forceinline__ void decode_sector(const BpArgs& a, Lane& ln, long lo
         for (int l = 0; l < L; ++l) msg[r][l] = pp;
 
     const float one_minus_pp = 1.0f - pp;
+    bool hard = false;  // the initial messages p' are not hard (0 < p' < 1 is required anyway)
     const int N = a.maxIter;
     bool active = in_range;  // group-uniform
     int it = 0;
@@ -528,12 +597,12 @@ __device__ __forceinline__ void decode_sector(const BpArgs& a, Lane& ln, long lo
         }
         if (active) {
             ++it;
-            if (iteration<R, L, SEC, STOP, false, SH, TU>(a, msg, sbits, n, ln, pp, one_minus_pp)) active = false;
+            if (iteration<R, L, SEC, STOP, false, SH, TU>(a, msg, sbits, n, ln, pp, one_minus_pp, hard)) active = false;
         }
     }
     if (n == N - 1 && active) {
         ++it;
-        iteration<R, L, SEC, STOP, true, SH, TU>(a, msg, sbits, n, ln, pp, one_minus_pp);
+        iteration<R, L, SEC, STOP, true, SH, TU>(a, msg, sbits, n, ln, pp, one_minus_pp, hard);
     }
 
     // ---- post-processing of Decode (DecoderCPU.h:354-384) ----
@@ -628,8 +697,8 @@ static Variant make_variant(int P, int S, int T, const char* name)
                     bp_decode_kernel<J, K, L, QEC_STOP_SYNDROME, SH, TU>},
                    name};
 }
-// Tune<min waves per SIMD, relabel, zero-skip, short division>
-template <int J, int K, int L, class TU = Tune<1, false, true, true>>
+// Tune<min waves per SIMD, relabel, zero-skip, short division, hard-message paths>
+template <int J, int K, int L, class TU = Tune<1, false, true, true, true>>
 static Variant rt()
 {
     return make_variant<J, K, L, RuntimeShifts, TU>(0, 0, 0, "wave-circulant runtime-shift");
@@ -643,21 +712,22 @@ static Variant gen()
 
 // Measured per variant with tools/kbench (profiles/r01/): P61 4 waves + relabel + zero-skip +
 // short division 7.11 ms vs 9.46 ms without them; P7 (9 syndromes per wave, so whole-wave
-// zero columns are rare) keeps 8 waves and only the short division.
+// zero columns are rare) keeps 8 waves and only the short division.  The hard-message paths:
+// P61 @ p=0.01 6.24 vs 7.28 ms, @ p=0.05 7.22 vs 9.36 ms; P7 0.186 vs 0.199 ms (session-3 kbench).
 static const Variant kVariants[] = {
     // specialised: the two code files the reference ships
-    gen<4, 5, 10, 61, 9, 49, Tune<4, true, true, true>>(),
-    gen<3, 3, 6, 7, 2, 3, Tune<8, false, false, true>>(),
+    gen<4, 5, 10, 61, 9, 49, Tune<4, true, true, true, true>>(),
+    gen<3, 3, 6, 7, 2, 3, Tune<8, false, false, true, true>>(),
 #ifndef QEC_KBENCH_MINIMAL  // experiment builds (tools/kbench) only compile the shipped-code kernels
     // runtime shifts, any P <= 64 with these block shapes
     rt<4, 5, 10>(),
-    rt<3, 3, 6, Tune<6, false, false, true>>(),
-    rt<2, 3, 6, Tune<6, false, false, true>>(),
+    rt<3, 3, 6, Tune<6, false, false, true, true>>(),
+    rt<2, 3, 6, Tune<6, false, false, true, true>>(),
     rt<3, 4, 8>(),
     rt<4, 4, 8>(),
     rt<3, 5, 10>(),
     rt<4, 6, 12>(),
-    rt<2, 2, 4, Tune<8, false, false, true>>(),
+    rt<2, 2, 4, Tune<8, false, false, true, true>>(),
 #endif
 };
 
@@ -687,7 +757,7 @@ const void* select_variant(const Code& c, std::string& name)
 
 int launch_decode(const void* variant, const Code& c, const uint8_t* sX, const uint8_t* sZ, long long B,
                   float errorProbability, int maxIter, int stop, uint8_t* eX, uint8_t* eZ, uint8_t* flags,
-                  int32_t* iters, float* q, hipStream_t stream)
+                  int32_t* iters, float* q, int hardPaths, hipStream_t stream)
 {
     const Variant* v = static_cast<const Variant*>(variant);
     if (B <= 0) return QEC_OK;
@@ -700,6 +770,7 @@ int launch_decode(const void* variant, const Code& c, const uint8_t* sX, const u
     a.errorProbability = errorProbability;
     a.maxIter = maxIter < 0 ? 0 : maxIter;
     a.stop = stop;
+    a.hardPaths = hardPaths;
     relabel(c.EX.data(), c.J, c.L, c.P, v->relabel, a.SX, a.DX, a.CX);
     relabel(c.EZ.data(), c.K, c.L, c.P, v->relabel, a.SZ, a.DZ, a.CZ);
     const int wavesPerBlock = QEC_WAVES_PER_BLOCK;

@@ -16,7 +16,7 @@ const char* last_error_cstr();
 const void* select_variant(const Code& c, std::string& name);
 int launch_decode(const void* variant, const Code& c, const uint8_t* sX, const uint8_t* sZ, long long B,
                   float errorProbability, int maxIter, int stop, uint8_t* eX, uint8_t* eZ, uint8_t* flags,
-                  int32_t* iters, float* q, hipStream_t stream);
+                  int32_t* iters, float* q, int hardPaths, hipStream_t stream);
 int launch_sample_depolarizing(uint64_t seed, uint64_t start, long long B, int n, float p, uint8_t* x, uint8_t* z,
                                hipStream_t st);
 int launch_errors_from_draws(const int32_t* idx, const uint8_t* type, long long B, int W, int n, uint8_t* x,
@@ -47,6 +47,7 @@ struct qec_decoder {
     const void* variant = nullptr;  // wave-circulant kernel variant (bp_decode.hip)
     void* sparse = nullptr;         // sparse-graph plan (bp_sparse.hip)
     std::string variant_name;
+    int hard_paths = 1;             // QEC_OPT_HARD_PATHS
     hipStream_t stream = nullptr;
     // staging for the host-pointer entry point (DecoderGPU's device vectors, DecoderGPU.h:28-35)
     DeviceArray<uint8_t> sX, sZ, eX, eZ, flags;
@@ -232,12 +233,31 @@ int qec_decoder_describe(const qec_decoder* d, char* buf, size_t len)
     return QEC_OK;
 }
 
+int qec_decoder_set_option(qec_decoder* d, int option, int value)
+{
+    if (!d) return fail(QEC_ERR_ARG, "qec_decoder_set_option: null decoder");
+    switch (option) {
+    case QEC_OPT_HARD_PATHS: d->hard_paths = value != 0; return QEC_OK;
+    default: return fail(QEC_ERR_ARG, "qec_decoder_set_option: unknown option");
+    }
+}
+
+int qec_decoder_get_option(const qec_decoder* d, int option, int* value)
+{
+    if (!d || !value) return fail(QEC_ERR_ARG, "qec_decoder_get_option: bad argument");
+    switch (option) {
+    case QEC_OPT_HARD_PATHS: *value = d->hard_paths; return QEC_OK;
+    default: return fail(QEC_ERR_ARG, "qec_decoder_get_option: unknown option");
+    }
+}
+
 static int dispatch_decode(qec_decoder* d, const uint8_t* sX, const uint8_t* sZ, long long B, float p, int maxIter,
                            int stop, uint8_t* eX, uint8_t* eZ, uint8_t* flags, int32_t* iters, float* q, hipStream_t st)
 {
     if (d->engine == QEC_ENGINE_SPARSE)
         return launch_decode_sparse(d->sparse, sX, sZ, B, p, maxIter, stop, eX, eZ, flags, iters, q, st);
-    return launch_decode(d->variant, *d->code, sX, sZ, B, p, maxIter, stop, eX, eZ, flags, iters, q, st);
+    return launch_decode(d->variant, *d->code, sX, sZ, B, p, maxIter, stop, eX, eZ, flags, iters, q, d->hard_paths,
+                         st);
 }
 
 static const int32_t* syndrome_table(const qec_decoder* d)

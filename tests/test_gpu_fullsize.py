@@ -76,3 +76,15 @@ def test_flags_consistent_with_syndromes(run):
     assert (iters == run["N"]).all()
     # the decoder actually decodes: most low-p samples satisfy their syndromes
     assert synx.mean() < 0.5 and synz.mean() < 0.5
+
+
+def test_hard_paths_off_identical(run):
+    """The bench's full-size batch decodes to the same bits with the hard-message paths off."""
+    dec = run["dec"]
+    dec.set_option("hard_paths", 0)
+    try:
+        off = dec.decode_batch(run["sX"], run["sZ"], run["p"], run["N"], "fixed", want_iters=True)
+    finally:
+        dec.set_option("hard_paths", 1)
+    for a, b in zip(run["out"][:4], off[:4]):
+        assert np.array_equal(a, b)

@@ -156,3 +156,27 @@ def test_runtime_shift_kernel_on_shipped_code(env, code_paths):
     for x, y in zip(a[:4], b[:4]):
         assert np.array_equal(x, y)
     assert same_floats(a[4], b[4])
+
+
+@pytest.mark.parametrize("key", ["P7", "P61"])
+@pytest.mark.parametrize("p", [0.001, 0.01, 0.05, 0.1])
+def test_hard_paths_bit_identical(env, key, p):
+    """QEC_OPT_HARD_PATHS (the exact hard-message forms of both updates, taken once every
+    message of a sector is +0 or 1.0) changes no output bit: decisions, flags, iteration
+    counts and final messages with the option on equal those with it off, and both equal
+    the oracle.  Low p saturates almost every sector within a few iterations; high p
+    leaves many sectors soft or NaN (0/0 in VarNodeUpdate), which must stay off the path."""
+    code, dec, _ = env[key]
+    x, z = depolarizing_errors(code.n, 777, 384, p)
+    sX, sZ = code.syndrome(0, x), code.syndrome(1, z)
+    assert dec.get_option("hard_paths") == 1
+    for stop in ("fixed", "ref", "syndrome"):
+        on = check(env, key, sX, sZ, p, 50, stop)
+        dec.set_option("hard_paths", 0)
+        try:
+            off = dec.decode_batch(sX, sZ, p, 50, stop, want_iters=True, want_q=True)
+        finally:
+            dec.set_option("hard_paths", 1)
+        for a, b in zip(on[:4], off[:4]):
+            assert np.array_equal(a, b)
+        assert same_floats(on[4], off[4])

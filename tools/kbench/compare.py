@@ -44,11 +44,14 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--stop", type=int, default=1)
     ap.add_argument("--iters", type=int, default=None)
+    ap.add_argument("--p", type=float, default=None, help="depolarising rate (default: the code's bench p)")
     ap.add_argument("variants", nargs="+")
     a = ap.parse_args()
     name, p, iters = CODES[a.code]
     if a.iters is not None:
         iters = a.iters
+    if a.p is not None:
+        p = a.p
     dev = torch.device("cuda", 0)
     libs = {v: bind(os.path.join(ROOT, "build", "variants", v, "libqecldpc.so")) for v in a.variants}
     first = libs[a.variants[0]]

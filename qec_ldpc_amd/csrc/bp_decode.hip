@@ -70,6 +70,10 @@ namespace qec {
 #ifndef QEC_SATURATE
 #define QEC_SATURATE -1
 #endif
+//   QEC_AGREE        0: hard sectors skip the whole-sector agreement test (var_pass_agree)
+#ifndef QEC_AGREE
+#define QEC_AGREE 1
+#endif
 #define QEC_PICK(macro, dflt) ((macro) >= 0 ? (macro) != 0 : (dflt))
 
 // Per-variant tuning: minimum waves per SIMD for the register allocator, and the options above.
@@ -503,6 +507,31 @@ __device__ __forceinline__ uint32_t var_pass(const BpArgs& a, float (&msg)[R][L]
     return hdmask;
 }
 
+// VarNodeUpdate on a hard sector whose R incoming messages agree for every variable (every
+// live lane): then each outgoing message q_j = P1 / (P0 + P1) is the common value (all 1:
+// p'/p' = 1; all 0: +0/(1-p') = +0; LAST or R >= 2, see var_pass), so the message sent back on
+// edge (r, l) equals the one that arrived on it and the check-view registers are already the
+// result.  Gathers every edge into the variable view and tests the agreement; returns false
+// (registers untouched) when some variable's inputs differ, and the caller runs var_pass.
+template <int R, int L, int SEC, bool HD, class SH>
+__device__ __forceinline__ bool var_pass_agree(const BpArgs& a, const float (&msg)[R][L], const Lane& ln,
+                                               uint32_t& hdmask)
+{
+    const int* et = SH::template table<SEC>(a);
+    bool same = true;
+    uint32_t hd = 0;
+#pragma unroll
+    for (int l = 0; l < L; ++l) {
+        const uint32_t x0 = __float_as_uint(rot<SH>(msg[0][l], ln, SH::template shift<SEC, L>(et, 0, l)));
+#pragma unroll
+        for (int r = 1; r < R; ++r)
+            same &= __float_as_uint(rot<SH>(msg[r][l], ln, SH::template shift<SEC, L>(et, r, l))) == x0;
+        if constexpr (HD) hd |= (uint32_t)(x0 == 0x3F800000u) << l;  // q >= 0.5f <=> q == 1.0f here
+    }
+    hdmask = hd;
+    return all_live(same, ln.live);
+}
+
 // CheckConvergence (DecoderCPU.h:231-246) on this lane's edges.
 template <int R, int L>
 __device__ __forceinline__ bool lane_converged(const float (&msg)[R][L])
@@ -546,12 +575,16 @@ __device__ __forceinline__ bool iteration(const BpArgs& a, float (&msg)[R][L], u
     // launder the permute bases so their per-rotation selects are recomputed inside the
     // loop instead of being hoisted into ~2 R L live registers
     if constexpr (QEC_MASK_SELECT) asm volatile("" : "+v"(ln.b0), "+v"(ln.b1));
-    if (TU::kSaturate && hard)
+    constexpr bool HD = STOP == QEC_STOP_SYNDROME;
+    uint32_t hdmask = 0;
+    if (TU::kSaturate && hard) {
         check_pass_hard<R, L>(msg, sbits);  // outputs are hard too: hard stays set for the var pass
-    else
+        if (!(QEC_AGREE && (LAST || R >= 2) && var_pass_agree<R, L, SEC, HD, SH>(a, msg, ln, hdmask)))
+            hdmask = var_pass<R, L, SEC, LAST, HD, SH, TU>(a, msg, ln, pp, one_minus_pp, hard);
+    } else {
         check_pass<R, L>(msg, sbits);
-    const uint32_t hdmask =
-        var_pass<R, L, SEC, LAST, STOP == QEC_STOP_SYNDROME, SH, TU>(a, msg, ln, pp, one_minus_pp, hard);
+        hdmask = var_pass<R, L, SEC, LAST, HD, SH, TU>(a, msg, ln, pp, one_minus_pp, hard);
+    }
     if constexpr (STOP == QEC_STOP_REF) {
         if (n % 10 == 0) return group_all(lane_converged<R, L>(msg), ln.gb, P);  // DecoderCPU.h:287-290
     } else if constexpr (STOP == QEC_STOP_SYNDROME) {

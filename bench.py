@@ -16,6 +16,8 @@ Prints one JSON line (rank 0).  Extra objects:
   full_arithmetic -- the same batch re-timed with QEC_OPT_HARD_PATHS off (every
                    iteration in full fp32 arithmetic, no hard-message forms), with a
                    bit-identity check against the timed run's outputs.
+  no_cycle_jump -- the same with only QEC_OPT_CYCLE_JUMP off (hard-message forms, but
+                   every iteration executed one by one), also bit-identity checked.
   valu          -- analytical full-arithmetic VALU lane-ops per launch over the
                    full_arithmetic launch time, vs the fp32 VALU issue ceiling (on the
                    hard-path launch the analytical count would over-count the work).
@@ -163,8 +165,10 @@ def main():
     achieved_gbs = bytes_per_syn * B / (kernel_ms * 1e-3) / 1e9
     ops = lane_ops_per_syndrome(code, 1) * (it_mean[0] + it_mean[1]) / 2.0
     full = None
+    nojump = None
     if args.hard_paths and not args.no_full_arith:
         full = full_arithmetic(dec, step, stream, B, (eX, eZ, fl, its))
+        nojump = full_arithmetic(dec, step, stream, B, (eX, eZ, fl, its), option="cycle_jump")
     # the analytical count is the full-arithmetic work: only a launch without the
     # hard-message paths can be priced against it
     valu_ms = full["kernel_ms"] if full else (kernel_ms if not args.hard_paths else None)
@@ -208,6 +212,7 @@ def main():
     }
     if full:
         out["full_arithmetic"] = full
+        out["no_cycle_jump"] = nojump
     if args.stop != "fixed":
         hist = np.bincount(it_np.ravel(), minlength=iters + 1)
         out["iteration_histogram"] = {str(k): int(v) for k, v in enumerate(hist) if v}
@@ -221,11 +226,13 @@ def main():
         print(json.dumps(out), flush=True)
 
 
-def full_arithmetic(dec, step, stream, B, outs, reps=3):
-    """Re-time the step with the hard-message paths off and check the outputs are the same bits."""
+def full_arithmetic(dec, step, stream, B, outs, reps=3, option="hard_paths"):
+    """Re-time the step with a shortcut option off (hard_paths: every iteration in full
+    arithmetic; cycle_jump: hard iterations run one by one) and check the outputs are the
+    same bits."""
     import torch
     ref = [t.clone() for t in outs]
-    dec.set_option("hard_paths", 0)
+    dec.set_option(option, 0)
     try:
         step()
         ms = []
@@ -237,7 +244,7 @@ def full_arithmetic(dec, step, stream, B, outs, reps=3):
             torch.cuda.synchronize()
             ms.append(a.elapsed_time(b))
     finally:
-        dec.set_option("hard_paths", 1)
+        dec.set_option(option, 1)
     same = all(torch.equal(r, t) for r, t in zip(ref, outs))
     k = float(np.median(ms))
     return {"kernel_ms": round(k, 4), "syndromes_per_s": round(B / k * 1e3, 1), "identical": bool(same)}

@@ -126,8 +126,13 @@ int qec_decoder_destroy(qec_decoder* dec);
  *   QEC_OPT_HARD_PATHS (default 1): once every message of a sector is exactly +0 or 1.0 the
  *     wave-circulant kernels switch to the exact hard-message forms of the check and variable
  *     updates (bp_decode.hip, check_pass_hard / var_pass).  Outputs are bit-identical either
- *     way; 0 forces the full arithmetic every iteration (for measurement). */
-enum { QEC_OPT_HARD_PATHS = 1 };
+ *     way; 0 forces the full arithmetic every iteration (for measurement).
+ *   QEC_OPT_CYCLE_JUMP (default 1; needs QEC_OPT_HARD_PATHS): once two consecutive iterations
+ *     of a hard sector return every variable's inputs unchanged, the remaining iterations
+ *     provably alternate between the two states just computed (bp_decode.hip, cycle_end), so
+ *     the kernel jumps to the sector's last iteration.  Bit-identical either way; 0 runs the
+ *     remaining hard iterations one by one (for measurement). */
+enum { QEC_OPT_HARD_PATHS = 1, QEC_OPT_CYCLE_JUMP = 2 };
 int qec_decoder_set_option(qec_decoder* dec, int option, int value);
 int qec_decoder_get_option(const qec_decoder* dec, int option, int* value);
 /* which kernel variant serves this code: writes a short name (e.g. "wave-circulant P=61 G=1") */

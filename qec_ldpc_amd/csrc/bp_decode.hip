@@ -110,7 +110,7 @@ struct BpArgs {
     int P, G, n, mX, mZ;
     float errorProbability;
     int maxIter, stop;
-    int hardPaths;  // 0 disables the hard-message paths of variants compiled with them (QEC_OPT_HARD_PATHS)
+    int hardPaths;  // QEC_HP_* bits: hard-message paths / cycle jump (QEC_OPT_HARD_PATHS, QEC_OPT_CYCLE_JUMP)
     // lane-relabelled circulant tables (see relabel() below)
     int SX[kMaxRL], SZ[kMaxRL];  // rotation of block (r, l) between check and variable views
     int DX[kMaxR], DZ[kMaxR];    // check-view lane lambda holds check (r, (lambda + D[r]) mod P)
@@ -503,7 +503,7 @@ __device__ __forceinline__ uint32_t var_pass(const BpArgs& a, float (&msg)[R][L]
             msg[r][l] = rot<SH>(qv[r], ln, sh == 0 ? 0 : P - sh);
         }
     }
-    if constexpr (TU::kSaturate) hard = a.hardPaths != 0 && hard_ok(pp) && all_live(soft_bits == 0u, ln.live);
+    if constexpr (TU::kSaturate) hard = (a.hardPaths & QEC_HP_FORMS) && hard_ok(pp) && all_live(soft_bits == 0u, ln.live);
     return hdmask;
 }
 
@@ -567,9 +567,11 @@ __device__ __forceinline__ bool lane_syndrome_ok(const BpArgs& a, uint32_t hdmas
 
 // One BP iteration; returns true if this group stops after it.
 // hard: every variable->check message of this sector is exactly +0 or 1.0 (wave-uniform).
+// agreed: set when the iteration took the agreement path (hard sector, every variable's inputs
+// equal), i.e. it mapped msg to check_pass_hard(msg) (wave-uniform).
 template <int R, int L, int SEC, int STOP, bool LAST, class SH, class TU>
 __device__ __forceinline__ bool iteration(const BpArgs& a, float (&msg)[R][L], uint32_t sbits, int n, Lane& ln,
-                                          float pp, float one_minus_pp, bool& hard)
+                                          float pp, float one_minus_pp, bool& hard, bool& agreed)
 {
     const int P = SH::P(a);
     // launder the permute bases so their per-rotation selects are recomputed inside the
@@ -577,10 +579,11 @@ __device__ __forceinline__ bool iteration(const BpArgs& a, float (&msg)[R][L], u
     if constexpr (QEC_MASK_SELECT) asm volatile("" : "+v"(ln.b0), "+v"(ln.b1));
     constexpr bool HD = STOP == QEC_STOP_SYNDROME;
     uint32_t hdmask = 0;
+    agreed = false;
     if (TU::kSaturate && hard) {
         check_pass_hard<R, L>(msg, sbits);  // outputs are hard too: hard stays set for the var pass
-        if (!(QEC_AGREE && (LAST || R >= 2) && var_pass_agree<R, L, SEC, HD, SH>(a, msg, ln, hdmask)))
-            hdmask = var_pass<R, L, SEC, LAST, HD, SH, TU>(a, msg, ln, pp, one_minus_pp, hard);
+        agreed = QEC_AGREE && (LAST || R >= 2) && var_pass_agree<R, L, SEC, HD, SH>(a, msg, ln, hdmask);
+        if (!agreed) hdmask = var_pass<R, L, SEC, LAST, HD, SH, TU>(a, msg, ln, pp, one_minus_pp, hard);
     } else {
         check_pass<R, L>(msg, sbits);
         hdmask = var_pass<R, L, SEC, LAST, HD, SH, TU>(a, msg, ln, pp, one_minus_pp, hard);
@@ -591,6 +594,29 @@ __device__ __forceinline__ bool iteration(const BpArgs& a, float (&msg)[R][L], u
         return group_all(lane_syndrome_ok<R, L, SEC, SH>(a, hdmask, sbits, ln), ln.gb, P);
     }
     return false;
+}
+
+// ---- cycle jump --------------------------------------------------------------
+// On a hard sector the agreement path maps the check-view registers q to F(q) = check_pass_hard(q):
+// row r becomes q ^ c_r with c_r = s_r ^ XOR_l q[r][l] (on the bit patterns {0, 1.0f}).  Then
+//   L even: XOR_l F(q)[r][l] = XOR_l q[r][l], so c_r(F(q)) = c_r(q) and F(F(q)) = q;
+//   L odd:  c_r(F(q)) = 0, so F(F(q)) = F(q).
+// So once two consecutive iterations n-1, n take the agreement path (states S_n = F(S_{n-1}) and
+// S_{n+1} = F(S_n) both pass the agreement test), every later state is S_n or S_{n+1}: each passes
+// the test again, every later iteration (the last one, with the self message, included: see
+// var_pass_agree) is F again, and F^k(S_{n+1}) = F^(k mod 2)(S_{n+1}).  The stop tests repeat
+// too: the syndrome rule tested both states already (and did not stop); the reference rule's
+// convergence test holds on every hard state, so it stops at the next n' with n' % 10 == 0.
+// The sector therefore jumps straight to its last executed iteration: same registers, same
+// iteration count, same flags as running the iterations one by one (bit-identical).
+template <int STOP>
+__device__ __forceinline__ int cycle_end(int n, int N)
+{
+    if constexpr (STOP == QEC_STOP_REF) {
+        const int next10 = (n / 10 + 1) * 10;  // DecoderCPU.h:287-290
+        return next10 < N - 1 ? next10 : N - 1;
+    }
+    return N - 1;
 }
 
 template <int R, int L, int SEC, int STOP, class SH, class TU>
@@ -623,19 +649,30 @@ __device__ __forceinline__ void decode_sector(const BpArgs& a, Lane& ln, long lo
     bool active = in_range;  // group-uniform
     int it = 0;
     int n = 0;
+    int agree_run = 0;  // consecutive iterations that took the agreement path (wave-uniform)
+    bool agreed = false;
     // iterations 0 .. N-2 (DecoderCPU.h:280-291); the last one is peeled below
     for (; n < N - 1; ++n) {
-        if constexpr (STOP != QEC_STOP_FIXED) {
-            if (!__any(active)) break;  // DecoderCPU.h:282
-        }
+        if (!__any(active)) break;  // DecoderCPU.h:282 (fixed: only after a cycle jump)
         if (active) {
             ++it;
-            if (iteration<R, L, SEC, STOP, false, SH, TU>(a, msg, sbits, n, ln, pp, one_minus_pp, hard)) active = false;
+            if (iteration<R, L, SEC, STOP, false, SH, TU>(a, msg, sbits, n, ln, pp, one_minus_pp, hard, agreed))
+                active = false;
+            if constexpr (TU::kSaturate) {
+                agree_run = agreed ? agree_run + 1 : 0;
+                if (agree_run >= 2 && active && (a.hardPaths & QEC_HP_CYCLE)) {
+                    const int last = cycle_end<STOP>(n, N);
+                    if ((last - n) & 1) check_pass_hard<R, L>(msg, sbits);
+                    it += last - n;
+                    active = false;
+                    n = N;  // skips the peeled last iteration too
+                }
+            }
         }
     }
     if (n == N - 1 && active) {
         ++it;
-        iteration<R, L, SEC, STOP, true, SH, TU>(a, msg, sbits, n, ln, pp, one_minus_pp, hard);
+        iteration<R, L, SEC, STOP, true, SH, TU>(a, msg, sbits, n, ln, pp, one_minus_pp, hard, agreed);
     }
 
     // ---- post-processing of Decode (DecoderCPU.h:354-384) ----

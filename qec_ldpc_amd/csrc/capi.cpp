@@ -48,6 +48,7 @@ struct qec_decoder {
     void* sparse = nullptr;         // sparse-graph plan (bp_sparse.hip)
     std::string variant_name;
     int hard_paths = 1;             // QEC_OPT_HARD_PATHS
+    int cycle_jump = 1;             // QEC_OPT_CYCLE_JUMP
     hipStream_t stream = nullptr;
     // staging for the host-pointer entry point (DecoderGPU's device vectors, DecoderGPU.h:28-35)
     DeviceArray<uint8_t> sX, sZ, eX, eZ, flags;
@@ -238,6 +239,7 @@ int qec_decoder_set_option(qec_decoder* d, int option, int value)
     if (!d) return fail(QEC_ERR_ARG, "qec_decoder_set_option: null decoder");
     switch (option) {
     case QEC_OPT_HARD_PATHS: d->hard_paths = value != 0; return QEC_OK;
+    case QEC_OPT_CYCLE_JUMP: d->cycle_jump = value != 0; return QEC_OK;
     default: return fail(QEC_ERR_ARG, "qec_decoder_set_option: unknown option");
     }
 }
@@ -247,6 +249,7 @@ int qec_decoder_get_option(const qec_decoder* d, int option, int* value)
     if (!d || !value) return fail(QEC_ERR_ARG, "qec_decoder_get_option: bad argument");
     switch (option) {
     case QEC_OPT_HARD_PATHS: *value = d->hard_paths; return QEC_OK;
+    case QEC_OPT_CYCLE_JUMP: *value = d->cycle_jump; return QEC_OK;
     default: return fail(QEC_ERR_ARG, "qec_decoder_get_option: unknown option");
     }
 }
@@ -256,8 +259,8 @@ static int dispatch_decode(qec_decoder* d, const uint8_t* sX, const uint8_t* sZ,
 {
     if (d->engine == QEC_ENGINE_SPARSE)
         return launch_decode_sparse(d->sparse, sX, sZ, B, p, maxIter, stop, eX, eZ, flags, iters, q, st);
-    return launch_decode(d->variant, *d->code, sX, sZ, B, p, maxIter, stop, eX, eZ, flags, iters, q, d->hard_paths,
-                         st);
+    const int hp = d->hard_paths ? (QEC_HP_FORMS | (d->cycle_jump ? QEC_HP_CYCLE : 0)) : 0;
+    return launch_decode(d->variant, *d->code, sX, sZ, B, p, maxIter, stop, eX, eZ, flags, iters, q, hp, st);
 }
 
 static const int32_t* syndrome_table(const qec_decoder* d)

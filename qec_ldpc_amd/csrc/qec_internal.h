@@ -9,6 +9,9 @@
 
 namespace qec {
 
+// BpArgs::hardPaths bits (from QEC_OPT_HARD_PATHS / QEC_OPT_CYCLE_JUMP)
+enum { QEC_HP_FORMS = 1, QEC_HP_CYCLE = 2 };
+
 // Thread-local last-error text behind qec_last_error().
 void set_error(const std::string& msg);
 int fail(int status, const std::string& msg);

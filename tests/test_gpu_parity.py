@@ -180,3 +180,25 @@ def test_hard_paths_bit_identical(env, key, p):
         for a, b in zip(on[:4], off[:4]):
             assert np.array_equal(a, b)
         assert same_floats(on[4], off[4])
+
+
+@pytest.mark.parametrize("key", ["P7", "P61"])
+@pytest.mark.parametrize("N", [5, 7, 11, 12, 20, 21, 33])
+def test_cycle_jump_bit_identical(env, key, N):
+    """QEC_OPT_CYCLE_JUMP (a hard sector whose last two iterations agreed jumps to its last
+    iteration, bp_decode.hip cycle_end) changes no output bit: even and odd remaining counts,
+    the reference rule's next multiple of 10 before and after N - 1, every stop rule.  The
+    jump on equals the jump off, and both equal the oracle (final messages included)."""
+    code, dec, _ = env[key]
+    x, z = depolarizing_errors(code.n, 4242 + N, 256, 0.01)
+    sX, sZ = code.syndrome(0, x), code.syndrome(1, z)
+    for stop in ("fixed", "ref", "syndrome"):
+        on = check(env, key, sX, sZ, 0.01, N, stop)
+        dec.set_option("cycle_jump", 0)
+        try:
+            off = dec.decode_batch(sX, sZ, 0.01, N, stop, want_iters=True, want_q=True)
+        finally:
+            dec.set_option("cycle_jump", 1)
+        for a, b in zip(on[:4], off[:4]):
+            assert np.array_equal(a, b)
+        assert same_floats(on[4], off[4])

@@ -18,6 +18,7 @@ from qec_ldpc_amd.codes import P7, P61, code_path  # noqa: E402
 from qec_ldpc_amd.synthetic import depolarizing_errors  # noqa: E402
 
 CODES = {"p61": (P61, 0.01, 50), "p7": (P7, 0.02, 20)}
+OPTIONS = {"hard_paths": 1, "cycle_jump": 2}
 
 
 def bind(path):
@@ -34,6 +35,7 @@ def bind(path):
     L.qec_code_params.argtypes = [vp, vp]
     L.qec_decoder_describe.argtypes = [vp, ctypes.c_char_p, ctypes.c_size_t]
     L.qec_last_error.restype = ctypes.c_char_p
+    L.qec_decoder_set_option.argtypes = [vp, ctypes.c_int, ctypes.c_int]
     return L
 
 
@@ -53,7 +55,10 @@ def main():
     if a.p is not None:
         p = a.p
     dev = torch.device("cuda", 0)
-    libs = {v: bind(os.path.join(ROOT, "build", "variants", v, "libqecldpc.so")) for v in a.variants}
+    # a variant is "<build dir>" or "<build dir>:<option>=<value>,..." (decoder options, e.g.
+    # cur:cycle_jump=0), so one build can be timed with several option settings
+    opts = {v: [kv.split("=") for kv in v.split(":", 1)[1].split(",")] if ":" in v else [] for v in a.variants}
+    libs = {v: bind(os.path.join(ROOT, "build", "variants", v.split(":")[0], "libqecldpc.so")) for v in a.variants}
     first = libs[a.variants[0]]
     ch = first.qec_code_load(code_path(name).encode())
     prm = np.zeros(9, np.int32)
@@ -73,6 +78,8 @@ def main():
         d = L.qec_decoder_create(c, 0, 0)
         if not d:
             raise SystemExit("%s: %s" % (v, L.qec_last_error()))
+        for k, val in opts[v]:
+            assert L.qec_decoder_set_option(d, OPTIONS[k], int(val)) == 0, L.qec_last_error()
         buf = ctypes.create_string_buffer(256)
         L.qec_decoder_describe(d, buf, 256)
         decs[v] = (L, d, buf.value.decode())

@@ -131,8 +131,20 @@ int qec_decoder_destroy(qec_decoder* dec);
  *     of a hard sector return every variable's inputs unchanged, the remaining iterations
  *     provably alternate between the two states just computed (bp_decode.hip, cycle_end), so
  *     the kernel jumps to the sector's last iteration.  Bit-identical either way; 0 runs the
- *     remaining hard iterations one by one (for measurement). */
-enum { QEC_OPT_HARD_PATHS = 1, QEC_OPT_CYCLE_JUMP = 2 };
+ *     remaining hard iterations one by one (for measurement).
+ *   QEC_OPT_SCHEDULE (default 1): dispatch order of the wave-circulant launch.  Two small
+ *     kernels (a counting sort) order the batch by syndrome weight and the decode waves take syndromes heaviest
+ *     first, so the rare syndromes that run every iteration in full arithmetic start early
+ *     instead of extending the launch (schedule.hip).  Outputs are written at each syndrome's
+ *     own index and are bit-identical either way.  0 = batch order, 1 = sorted when
+ *     4096 <= B <= 2^22, 2 = sorted when B <= 2^22.  The workspace (5 B per syndrome + 1 MiB) is allocated
+ *     by qec_decoder_create for max_batch and grown on demand by larger calls.
+ *   QEC_OPT_SECTOR_SPLIT (default 1): the X and Z sectors of a syndrome are decoded by two
+ *     waves instead of one after the other (halves the longest wave).  The launch then zeroes
+ *     flags[] first and each sector ORs in its bits.  Bit-identical either way.  0 = off,
+ *     1 = the kernel variant's measured choice (on for P7, off for P61), 2 = on where the
+ *     variant has split kernels (the two shipped codes). */
+enum { QEC_OPT_HARD_PATHS = 1, QEC_OPT_CYCLE_JUMP = 2, QEC_OPT_SCHEDULE = 3, QEC_OPT_SECTOR_SPLIT = 4 };
 int qec_decoder_set_option(qec_decoder* dec, int option, int value);
 int qec_decoder_get_option(const qec_decoder* dec, int option, int* value);
 /* which kernel variant serves this code: writes a short name (e.g. "wave-circulant P=61 G=1") */

@@ -26,7 +26,7 @@ CONVERGENCE_FAIL_X = 4
 CONVERGENCE_FAIL_Z = 8
 STOP = {"ref": 0, "fixed": 1, "syndrome": 2}
 ENGINE = {"auto": 0, "circulant": 1, "sparse": 2}
-OPTION = {"hard_paths": 1, "cycle_jump": 2}
+OPTION = {"hard_paths": 1, "cycle_jump": 2, "schedule": 3, "sector_split": 4}
 
 # every symbol include/qec_ldpc.h declares
 EXPORTS = (

@@ -74,12 +74,18 @@ namespace qec {
 #ifndef QEC_AGREE
 #define QEC_AGREE 1
 #endif
+//   QEC_PHASE_STATS  experiment builds only: iters[] reports, per sector, the iterations spent in
+//                    each phase (soft | hard << 8 | agreed << 16 | jumped << 24) instead of the count
+#ifndef QEC_PHASE_STATS
+#define QEC_PHASE_STATS 0
+#endif
 #define QEC_PICK(macro, dflt) ((macro) >= 0 ? (macro) != 0 : (dflt))
 
 // Per-variant tuning: minimum waves per SIMD for the register allocator, and the options above.
-template <int MINW_, bool RELABEL_, bool ZEROSKIP_, bool FASTDIV_, bool SATURATE_ = false>
+template <int MINW_, bool RELABEL_, bool ZEROSKIP_, bool FASTDIV_, bool SATURATE_ = false, bool SPLIT_ = false>
 struct Tune {
     static constexpr int kMinWaves = MINW_;
+    static constexpr bool kSplit = SPLIT_;  // QEC_OPT_SECTOR_SPLIT = 1 (auto) splits sectors for this variant
     static constexpr bool kRelabel = QEC_PICK(QEC_RELABEL, RELABEL_);
     static constexpr bool kZeroSkip = QEC_PICK(QEC_ZEROSKIP, ZEROSKIP_);
     static constexpr bool kFastDiv = QEC_PICK(QEC_FASTDIV, FASTDIV_);
@@ -106,6 +112,7 @@ struct BpArgs {
     uint8_t* flags;
     int32_t* iters;
     float* q;
+    const int32_t* perm;  // dispatch order (schedule.hip): group slot k decodes syndrome perm[k]; null = batch order
     long long B;
     int P, G, n, mX, mZ;
     float errorProbability;
@@ -651,19 +658,23 @@ __device__ __forceinline__ void decode_sector(const BpArgs& a, Lane& ln, long lo
     int n = 0;
     int agree_run = 0;  // consecutive iterations that took the agreement path (wave-uniform)
     bool agreed = false;
+    int ph_soft = 0, ph_hard = 0, ph_agree = 0, ph_jump = 0;  // QEC_PHASE_STATS
     // iterations 0 .. N-2 (DecoderCPU.h:280-291); the last one is peeled below
     for (; n < N - 1; ++n) {
         if (!__any(active)) break;  // DecoderCPU.h:282 (fixed: only after a cycle jump)
         if (active) {
             ++it;
+            const bool was_hard = hard;
             if (iteration<R, L, SEC, STOP, false, SH, TU>(a, msg, sbits, n, ln, pp, one_minus_pp, hard, agreed))
                 active = false;
+            if constexpr (QEC_PHASE_STATS) { ph_soft += !was_hard; ph_hard += was_hard && !agreed; ph_agree += agreed; }
             if constexpr (TU::kSaturate) {
                 agree_run = agreed ? agree_run + 1 : 0;
                 if (agree_run >= 2 && active && (a.hardPaths & QEC_HP_CYCLE)) {
                     const int last = cycle_end<STOP>(n, N);
                     if ((last - n) & 1) check_pass_hard<R, L>(msg, sbits);
                     it += last - n;
+                    if constexpr (QEC_PHASE_STATS) ph_jump = last - n;
                     active = false;
                     n = N;  // skips the peeled last iteration too
                 }
@@ -672,7 +683,9 @@ __device__ __forceinline__ void decode_sector(const BpArgs& a, Lane& ln, long lo
     }
     if (n == N - 1 && active) {
         ++it;
+        const bool was_hard = hard;
         iteration<R, L, SEC, STOP, true, SH, TU>(a, msg, sbits, n, ln, pp, one_minus_pp, hard, agreed);
+        if constexpr (QEC_PHASE_STATS) { ph_soft += !was_hard; ph_hard += was_hard && !agreed; ph_agree += agreed; }
     }
 
     // ---- post-processing of Decode (DecoderCPU.h:354-384) ----
@@ -695,7 +708,7 @@ __device__ __forceinline__ void decode_sector(const BpArgs& a, Lane& ln, long lo
 
     if (!syn_ok) flags |= SEC ? QEC_SYNDROME_FAIL_Z : QEC_SYNDROME_FAIL_X;
     if (!conv) flags |= SEC ? QEC_CONVERGENCE_FAIL_Z : QEC_CONVERGENCE_FAIL_X;
-    iters_out = it;
+    iters_out = QEC_PHASE_STATS ? (ph_soft | ph_hard << 8 | ph_agree << 16 | ph_jump << 24) : it;
 
     if (a.q != nullptr && in_range) {
         const long long qb = b * (long long)(a.mX + a.mZ) * L + (SEC ? (long long)a.mX * L : 0);
@@ -717,7 +730,9 @@ __device__ __forceinline__ void decode_sector(const BpArgs& a, Lane& ln, long lo
 
 // MINW: minimum waves per SIMD the register allocator must allow (5 -> <= 96 VGPRs), measured
 // per variant with tools/kbench (P61: 5 waves beat 4 by 4 %; see profiles/).
-template <int RX, int RZ, int L, int STOP, class SH, class TU>
+// SPLIT: waves 2k and 2k+1 decode sectors X and Z of group k (adjacent waves, one workgroup);
+// the launch zeroed flags[] and each sector ORs in its bits.  Otherwise one wave decodes both.
+template <int RX, int RZ, int L, int STOP, class SH, class TU, bool SPLIT>
 __global__ __launch_bounds__(64 * QEC_WAVES_PER_BLOCK, (QEC_MIN_WAVES_PER_EU ? QEC_MIN_WAVES_PER_EU : TU::kMinWaves))
 void bp_decode_kernel(const BpArgs a)
 {
@@ -728,22 +743,32 @@ void bp_decode_kernel(const BpArgs a)
     const int g = lane / P;
     const int i = lane - g * P;
     const int gb = g * P;
-    const long long b = wave * G + g;
-    const bool in_range = (g < G) && (b < a.B);
+    const long long grp = SPLIT ? wave >> 1 : wave;
+    const long long slot = grp * G + g;
+    const bool in_range = (g < G) && (slot < a.B);
     if (!__any(in_range)) return;
+    const long long b = (in_range && a.perm != nullptr) ? (long long)a.perm[slot] : slot;
 
     // p' = (2/3) p, as the reference writes it (DecoderCPU.h:259)
     const float pp = 2.0f / 3.0f * a.errorProbability;
     uint32_t flags = 0;
     int itX = 0, itZ = 0;
     Lane ln{i, gb, 4 * (gb + i), 4 * (gb + i + P), in_range};
-    decode_sector<RX, L, 0, STOP, SH, TU>(a, ln, b, in_range, pp, flags, itX);
-    decode_sector<RZ, L, 1, STOP, SH, TU>(a, ln, b, in_range, pp, flags, itZ);
+    const bool doX = !SPLIT || (wave & 1) == 0;  // wave-uniform
+    if (doX) decode_sector<RX, L, 0, STOP, SH, TU>(a, ln, b, in_range, pp, flags, itX);
+    if (!doX || !SPLIT) decode_sector<RZ, L, 1, STOP, SH, TU>(a, ln, b, in_range, pp, flags, itZ);
     if (in_range && i == 0) {
-        a.flags[b] = (uint8_t)flags;
+        if constexpr (!SPLIT) {
+            a.flags[b] = (uint8_t)flags;
+        } else if (flags != 0) {
+            // OR this sector's bits into the byte through its aligned 32-bit word (the other
+            // three bytes of the word get | 0)
+            const uintptr_t addr = reinterpret_cast<uintptr_t>(a.flags + b);
+            atomicOr(reinterpret_cast<unsigned int*>(addr & ~(uintptr_t)3), flags << (8 * (addr & 3)));
+        }
         if (a.iters != nullptr) {
-            a.iters[2 * b] = itX;
-            a.iters[2 * b + 1] = itZ;
+            if (doX) a.iters[2 * b] = itX;
+            if (!doX || !SPLIT) a.iters[2 * b + 1] = itZ;
         }
     }
 }
@@ -755,29 +780,39 @@ struct Variant {
     int J, K, L;
     int P, sigma, tau;  // P > 0: specialised to the generator's tables for these parameters
     bool relabel;       // runtime-shift variants: relabel the lane tables at launch
+    bool split_auto;    // QEC_OPT_SECTOR_SPLIT = 1 takes the split kernels
     KernelFn fn[3];     // indexed by stop rule
+    KernelFn split[3];  // the same with one wave per sector (nullptr: not instantiated)
     const char* name;
 };
 
-template <int J, int K, int L, class SH, class TU>
+template <int J, int K, int L, class SH, class TU, bool WITH_SPLIT>
 static Variant make_variant(int P, int S, int T, const char* name)
 {
-    return Variant{J, K, L, P, S, T, TU::kRelabel,
-                   {bp_decode_kernel<J, K, L, QEC_STOP_REF, SH, TU>, bp_decode_kernel<J, K, L, QEC_STOP_FIXED, SH, TU>,
-                    bp_decode_kernel<J, K, L, QEC_STOP_SYNDROME, SH, TU>},
-                   name};
+    Variant v{J, K, L, P, S, T, TU::kRelabel, TU::kSplit && WITH_SPLIT,
+              {bp_decode_kernel<J, K, L, QEC_STOP_REF, SH, TU, false>,
+               bp_decode_kernel<J, K, L, QEC_STOP_FIXED, SH, TU, false>,
+               bp_decode_kernel<J, K, L, QEC_STOP_SYNDROME, SH, TU, false>},
+              {nullptr, nullptr, nullptr},
+              name};
+    if constexpr (WITH_SPLIT) {
+        v.split[QEC_STOP_REF] = bp_decode_kernel<J, K, L, QEC_STOP_REF, SH, TU, true>;
+        v.split[QEC_STOP_FIXED] = bp_decode_kernel<J, K, L, QEC_STOP_FIXED, SH, TU, true>;
+        v.split[QEC_STOP_SYNDROME] = bp_decode_kernel<J, K, L, QEC_STOP_SYNDROME, SH, TU, true>;
+    }
+    return v;
 }
 // Tune<min waves per SIMD, relabel, zero-skip, short division, hard-message paths>
 template <int J, int K, int L, class TU = Tune<1, false, true, true, true>>
 static Variant rt()
 {
-    return make_variant<J, K, L, RuntimeShifts, TU>(0, 0, 0, "wave-circulant runtime-shift");
+    return make_variant<J, K, L, RuntimeShifts, TU, false>(0, 0, 0, "wave-circulant runtime-shift");
 }
 template <int J, int K, int L, int P, int S, int T, class TU>
 static Variant gen()
 {
-    return make_variant<J, K, L, GeneratedShifts<J, K, L, P, S, T, TU::kRelabel>, TU>(P, S, T,
-                                                                                      "wave-circulant generated-shift");
+    return make_variant<J, K, L, GeneratedShifts<J, K, L, P, S, T, TU::kRelabel>, TU, true>(
+        P, S, T, "wave-circulant generated-shift");
 }
 
 // Measured per variant with tools/kbench (profiles/r01/): P61 4 waves + relabel + zero-skip +
@@ -787,7 +822,7 @@ static Variant gen()
 static const Variant kVariants[] = {
     // specialised: the two code files the reference ships
     gen<4, 5, 10, 61, 9, 49, Tune<4, true, true, true, true>>(),
-    gen<3, 3, 6, 7, 2, 3, Tune<8, false, false, true, true>>(),
+    gen<3, 3, 6, 7, 2, 3, Tune<8, false, false, true, true, true>>(),
 #ifndef QEC_KBENCH_MINIMAL  // experiment builds (tools/kbench) only compile the shipped-code kernels
     // runtime shifts, any P <= 64 with these block shapes
     rt<4, 5, 10>(),
@@ -827,12 +862,18 @@ const void* select_variant(const Code& c, std::string& name)
 
 int launch_decode(const void* variant, const Code& c, const uint8_t* sX, const uint8_t* sZ, long long B,
                   float errorProbability, int maxIter, int stop, uint8_t* eX, uint8_t* eZ, uint8_t* flags,
-                  int32_t* iters, float* q, int hardPaths, hipStream_t stream)
+                  int32_t* iters, float* q, int hardPaths, const int32_t* perm, int split, hipStream_t stream)
 {
     const Variant* v = static_cast<const Variant*>(variant);
     if (B <= 0) return QEC_OK;
     BpArgs a{};
     a.sX = sX; a.sZ = sZ; a.eX = eX; a.eZ = eZ; a.flags = flags; a.iters = iters; a.q = q;
+    a.perm = perm;
+    // QEC_OPT_SECTOR_SPLIT: 0 off, 1 the variant's tuned choice, 2 on (runtime-shift variants
+    // have no split kernels: one wave per syndrome)
+    split = (split == 2 || (split == 1 && v->split_auto)) && v->split[stop] != nullptr;
+    if (split && hipMemsetAsync(flags, 0, (size_t)B, stream) != hipSuccess)
+        return fail(QEC_ERR_HIP, "bp_decode: flags memset failed");
     a.B = B;
     a.P = c.P;
     a.G = 64 / c.P;
@@ -844,10 +885,10 @@ int launch_decode(const void* variant, const Code& c, const uint8_t* sX, const u
     relabel(c.EX.data(), c.J, c.L, c.P, v->relabel, a.SX, a.DX, a.CX);
     relabel(c.EZ.data(), c.K, c.L, c.P, v->relabel, a.SZ, a.DZ, a.CZ);
     const int wavesPerBlock = QEC_WAVES_PER_BLOCK;
-    const long long waves = (B + a.G - 1) / a.G;
+    const long long waves = (B + a.G - 1) / a.G * (split ? 2 : 1);
     const long long blocks = (waves + wavesPerBlock - 1) / wavesPerBlock;
     if (blocks > 0x7fffffffLL) return fail(QEC_ERR_ARG, "batch too large for one launch");
-    hipLaunchKernelGGL(v->fn[stop], dim3((unsigned)blocks), dim3(64 * wavesPerBlock), 0, stream, a);
+    hipLaunchKernelGGL(split ? v->split[stop] : v->fn[stop], dim3((unsigned)blocks), dim3(64 * wavesPerBlock), 0, stream, a);
     hipError_t err = hipGetLastError();
     if (err != hipSuccess) return fail(QEC_ERR_HIP, std::string("bp_decode launch: ") + hipGetErrorString(err));
     return QEC_OK;

@@ -16,7 +16,11 @@ const char* last_error_cstr();
 const void* select_variant(const Code& c, std::string& name);
 int launch_decode(const void* variant, const Code& c, const uint8_t* sX, const uint8_t* sZ, long long B,
                   float errorProbability, int maxIter, int stop, uint8_t* eX, uint8_t* eZ, uint8_t* flags,
-                  int32_t* iters, float* q, int hardPaths, hipStream_t stream);
+                  int32_t* iters, float* q, int hardPaths, const int32_t* perm, int split, hipStream_t stream);
+size_t schedule_workspace_bytes(long long B, int mX, int mZ);
+long long schedule_max_batch();
+int launch_schedule(const uint8_t* sX, const uint8_t* sZ, long long B, int mX, int mZ, void* ws, int32_t** perm_out,
+                    hipStream_t st);
 int launch_sample_depolarizing(uint64_t seed, uint64_t start, long long B, int n, float p, uint8_t* x, uint8_t* z,
                                hipStream_t st);
 int launch_errors_from_draws(const int32_t* idx, const uint8_t* type, long long B, int W, int n, uint8_t* x,
@@ -49,6 +53,9 @@ struct qec_decoder {
     std::string variant_name;
     int hard_paths = 1;             // QEC_OPT_HARD_PATHS
     int cycle_jump = 1;             // QEC_OPT_CYCLE_JUMP
+    int schedule = 1;               // QEC_OPT_SCHEDULE (0 off, 1 auto, 2 always)
+    int sector_split = 1;           // QEC_OPT_SECTOR_SPLIT (0 off, 1 auto, 2 on)
+    DeviceArray<uint8_t> sched;     // dispatch-order workspace (schedule.hip)
     hipStream_t stream = nullptr;
     // staging for the host-pointer entry point (DecoderGPU's device vectors, DecoderGPU.h:28-35)
     DeviceArray<uint8_t> sX, sZ, eX, eZ, flags;
@@ -191,8 +198,11 @@ qec_decoder* qec_decoder_create_engine(const qec_code* h, int device, size_t max
         fail(QEC_ERR_HIP, "hipStreamCreate failed");
         return nullptr;
     }
-    (void)max_batch;  // staging grows on demand
     try {
+        // the dispatch-order workspace is sized up front so that qec_decode_batch_dev allocates
+        // nothing for batches up to max_batch (graph capture); staging grows on demand
+        if (max_batch > 0 && d->variant && (long long)max_batch <= schedule_max_batch())
+            d->sched.reserve(schedule_workspace_bytes((long long)max_batch, d->code->mX, d->code->mZ));
         if (!d->code->imp_rows.empty()) {
             d->imp.reserve(d->code->imp_rows.size());
             if (hipMemcpy(d->imp.data(), d->code->imp_rows.data(), d->code->imp_rows.size() * sizeof(uint64_t),
@@ -240,6 +250,14 @@ int qec_decoder_set_option(qec_decoder* d, int option, int value)
     switch (option) {
     case QEC_OPT_HARD_PATHS: d->hard_paths = value != 0; return QEC_OK;
     case QEC_OPT_CYCLE_JUMP: d->cycle_jump = value != 0; return QEC_OK;
+    case QEC_OPT_SCHEDULE:
+        if (value < 0 || value > 2) return fail(QEC_ERR_ARG, "qec_decoder_set_option: QEC_OPT_SCHEDULE is 0, 1 or 2");
+        d->schedule = value;
+        return QEC_OK;
+    case QEC_OPT_SECTOR_SPLIT:
+        if (value < 0 || value > 2) return fail(QEC_ERR_ARG, "qec_decoder_set_option: QEC_OPT_SECTOR_SPLIT is 0, 1 or 2");
+        d->sector_split = value;
+        return QEC_OK;
     default: return fail(QEC_ERR_ARG, "qec_decoder_set_option: unknown option");
     }
 }
@@ -250,9 +268,15 @@ int qec_decoder_get_option(const qec_decoder* d, int option, int* value)
     switch (option) {
     case QEC_OPT_HARD_PATHS: *value = d->hard_paths; return QEC_OK;
     case QEC_OPT_CYCLE_JUMP: *value = d->cycle_jump; return QEC_OK;
+    case QEC_OPT_SCHEDULE: *value = d->schedule; return QEC_OK;
+    case QEC_OPT_SECTOR_SPLIT: *value = d->sector_split; return QEC_OK;
     default: return fail(QEC_ERR_ARG, "qec_decoder_get_option: unknown option");
     }
 }
+
+// QEC_OPT_SCHEDULE = 1 orders batches from this size on (below it the three extra launches
+// cost more than the tail they remove)
+constexpr long long kScheduleMinBatch = 4096;
 
 static int dispatch_decode(qec_decoder* d, const uint8_t* sX, const uint8_t* sZ, long long B, float p, int maxIter,
                            int stop, uint8_t* eX, uint8_t* eZ, uint8_t* flags, int32_t* iters, float* q, hipStream_t st)
@@ -260,7 +284,20 @@ static int dispatch_decode(qec_decoder* d, const uint8_t* sX, const uint8_t* sZ,
     if (d->engine == QEC_ENGINE_SPARSE)
         return launch_decode_sparse(d->sparse, sX, sZ, B, p, maxIter, stop, eX, eZ, flags, iters, q, st);
     const int hp = d->hard_paths ? (QEC_HP_FORMS | (d->cycle_jump ? QEC_HP_CYCLE : 0)) : 0;
-    return launch_decode(d->variant, *d->code, sX, sZ, B, p, maxIter, stop, eX, eZ, flags, iters, q, hp, st);
+    const int32_t* perm = nullptr;
+    if (B > 1 && B <= schedule_max_batch() && (d->schedule == 2 || (d->schedule == 1 && B >= kScheduleMinBatch))) {
+        try {
+            d->sched.reserve(schedule_workspace_bytes(B, d->code->mX, d->code->mZ));
+        } catch (const std::exception& ex) {
+            return fail(QEC_ERR_NOMEM, std::string("decode: dispatch-order workspace: ") + ex.what());
+        }
+        int32_t* pm = nullptr;
+        const int rc = launch_schedule(sX, sZ, B, d->code->mX, d->code->mZ, d->sched.data(), &pm, st);
+        if (rc) return rc;
+        perm = pm;
+    }
+    return launch_decode(d->variant, *d->code, sX, sZ, B, p, maxIter, stop, eX, eZ, flags, iters, q, hp, perm,
+                         d->sector_split, st);
 }
 
 static const int32_t* syndrome_table(const qec_decoder* d)

@@ -88,3 +88,18 @@ def test_hard_paths_off_identical(run):
         dec.set_option("hard_paths", 1)
     for a, b in zip(run["out"][:4], off[:4]):
         assert np.array_equal(a, b)
+
+
+def test_schedule_split_off_identical(run):
+    """The full-size batch decodes to the same bits in batch order, one wave per syndrome
+    (QEC_OPT_SCHEDULE = 0, QEC_OPT_SECTOR_SPLIT = 0), as with the defaults."""
+    dec = run["dec"]
+    dec.set_option("schedule", 0)
+    dec.set_option("sector_split", 0)
+    try:
+        off = dec.decode_batch(run["sX"], run["sZ"], run["p"], run["N"], "fixed", want_iters=True)
+    finally:
+        dec.set_option("schedule", 1)
+        dec.set_option("sector_split", 1)
+    for a, b in zip(run["out"][:4], off[:4]):
+        assert np.array_equal(a, b)

@@ -202,3 +202,72 @@ def test_cycle_jump_bit_identical(env, key, N):
         for a, b in zip(on[:4], off[:4]):
             assert np.array_equal(a, b)
         assert same_floats(on[4], off[4])
+
+
+@pytest.mark.parametrize("key", ["P7", "P61"])
+@pytest.mark.parametrize("schedule,split", [(0, 0), (0, 2), (2, 0), (2, 2)])
+@pytest.mark.parametrize("B", [1, 2, 383])
+def test_schedule_and_split_bit_identical(env, key, schedule, split, B):
+    """QEC_OPT_SCHEDULE (waves take syndromes heaviest-first, schedule.hip) and
+    QEC_OPT_SECTOR_SPLIT (X and Z of a syndrome in two waves, flags merged by atomicOr)
+    change only which wave decodes what: every output bit equals the oracle's under every
+    stop rule, for a single syndrome, two, and a ragged batch (P7 packs 9 per wave)."""
+    code, dec, _ = env[key]
+    sX, sZ = mixed_inputs(code, max(B, 4), 91 + B, 0.02)
+    sX, sZ = sX[:B], sZ[:B]
+    dec.set_option("schedule", schedule)
+    dec.set_option("sector_split", split)
+    try:
+        for stop, N in (("fixed", 21), ("ref", 50), ("syndrome", 30)):
+            check(env, key, sX, sZ, 0.02, N, stop)
+    finally:
+        dec.set_option("schedule", 1)
+        dec.set_option("sector_split", 1)
+
+
+@pytest.mark.parametrize("key", ["P7", "P61"])
+def test_split_flags_unaligned_and_dirty(env, key):
+    """With the sector split the launch zeroes flags[] and each sector ORs its bits into the
+    aligned 32-bit word that holds the byte: an output buffer that starts with garbage and
+    sits at an odd address must come out right, and the bytes either side must be untouched."""
+    import torch
+    code, dec, _ = env[key]
+    B = 301
+    sX, sZ = mixed_inputs(code, B, 5, 0.05)
+    dev = torch.device("cuda", 0)
+    ref = check(env, key, sX, sZ, 0.05, 20, "fixed", want_q=False)
+    tX, tZ = torch.from_numpy(sX).to(dev), torch.from_numpy(sZ).to(dev)
+    eX = torch.empty((B, code.n), dtype=torch.uint8, device=dev)
+    eZ = torch.empty((B, code.n), dtype=torch.uint8, device=dev)
+    for off in (0, 1, 2, 3):
+        buf = torch.full((B + 8,), 0xA5, dtype=torch.uint8, device=dev)
+        fl = buf[off:off + B]
+        dec.set_option("sector_split", 2)
+        try:
+            dec.decode_batch_dev(tX, tZ, 0.05, 20, "fixed", eX, eZ, fl)
+            torch.cuda.synchronize()
+        finally:
+            dec.set_option("sector_split", 1)
+        h = buf.cpu().numpy()
+        assert np.array_equal(h[off:off + B], ref[2]), "offset %d" % off
+        assert (h[:off] == 0xA5).all() and (h[off + B:] == 0xA5).all(), "offset %d: neighbours changed" % off
+        assert np.array_equal(eX.cpu().numpy(), ref[0]) and np.array_equal(eZ.cpu().numpy(), ref[1])
+
+
+@pytest.mark.parametrize("key", ["P7", "P61"])
+def test_schedule_many_chunks_identical(env, key):
+    """A ragged batch spread over many counting-sort chunks (schedule.hip) decodes to the
+    same bits sorted and in batch order."""
+    code, dec, _ = env[key]
+    B = 70001
+    x, z = depolarizing_errors(code.n, 99, B, 0.03)
+    sX, sZ = code.syndrome(0, x), code.syndrome(1, z)
+    outs = []
+    for sched in (2, 0):
+        dec.set_option("schedule", sched)
+        try:
+            outs.append(dec.decode_batch(sX, sZ, 0.03, 20, "ref", want_iters=True))
+        finally:
+            dec.set_option("schedule", 1)
+    for a, b in zip(outs[0][:4], outs[1][:4]):
+        assert np.array_equal(a, b)

@@ -13,12 +13,12 @@ for code in $CODES; do
   mkdir -p "$OUT/$code"
   if [ "$code" = "p7" ]; then IT=20; else IT=50; fi
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/$code/trace" -o run -- \
-      python3 "$R/bench.py" --no-cpu --steps 10 --warmup 2 --code "$code" > "$OUT/$code/bench_trace.json" 2> "$OUT/$code/trace.err"
+      python3 "$R/bench.py" --no-cpu --no-full-arith --steps 10 --warmup 2 --code "$code" > "$OUT/$code/bench_trace.json" 2> "$OUT/$code/trace.err"
   rc=$?; echo "$code trace rc=$rc"; cat "$OUT/$code/bench_trace.json"
   if [ $rc -ne 0 ]; then tail -5 "$OUT/$code/trace.err"; exit $rc; fi
   for ctr in FETCH_SIZE WRITE_SIZE; do
     timeout -k 10 -s KILL 120 rocprofv3 --kernel-trace --pmc $ctr --output-format csv -d "$OUT/$code/$ctr" -o run -- \
-        python3 "$R/bench.py" --no-cpu --steps 3 --warmup 1 --code "$code" > "$OUT/$code/bench_$ctr.json" 2> "$OUT/$code/$ctr.err"
+        python3 "$R/bench.py" --no-cpu --no-full-arith --steps 3 --warmup 1 --code "$code" > "$OUT/$code/bench_$ctr.json" 2> "$OUT/$code/$ctr.err"
     rc=$?; echo "$code $ctr rc=$rc"
     if [ $rc -ne 0 ]; then tail -5 "$OUT/$code/$ctr.err"; exit $rc; fi
   done

@@ -17,6 +17,7 @@ common qec_ldpc_amd/csrc/code_model.cpp -x c++ &
 common qec_ldpc_amd/csrc/montecarlo.hip &
 common qec_ldpc_amd/csrc/capi.cpp -x hip &
 common qec_ldpc_amd/csrc/bp_sparse.hip &
+common qec_ldpc_amd/csrc/schedule.hip &
 wait
 build() {
   name=$1; shift

@@ -127,11 +127,12 @@ int qec_decoder_destroy(qec_decoder* dec);
  *     wave-circulant kernels switch to the exact hard-message forms of the check and variable
  *     updates (bp_decode.hip, check_pass_hard / var_pass).  Outputs are bit-identical either
  *     way; 0 forces the full arithmetic every iteration (for measurement).
- *   QEC_OPT_CYCLE_JUMP (default 1; needs QEC_OPT_HARD_PATHS): once two consecutive iterations
- *     of a hard sector return every variable's inputs unchanged, the remaining iterations
- *     provably alternate between the two states just computed (bp_decode.hip, cycle_end), so
- *     the kernel jumps to the sector's last iteration.  Bit-identical either way; 0 runs the
- *     remaining hard iterations one by one (for measurement).
+ *   QEC_OPT_CYCLE_JUMP (default 1; needs QEC_OPT_HARD_PATHS): once a hard sector whose
+ *     variables all carry equal messages takes an iteration that leaves every variable's inputs
+ *     unchanged, the remaining iterations provably alternate between the two states just seen
+ *     (bp_decode.hip, cycle_end), so the kernel jumps to the sector's last iteration.
+ *     Bit-identical either way; 0 runs the remaining hard iterations one by one (for
+ *     measurement).
  *   QEC_OPT_SCHEDULE (default 1): dispatch order of the wave-circulant launch.  Two small
  *     kernels (a counting sort) order the batch by syndrome weight and the decode waves take syndromes heaviest
  *     first, so the rare syndromes that run every iteration in full arithmetic start early

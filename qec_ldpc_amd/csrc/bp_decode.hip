@@ -79,6 +79,10 @@ namespace qec {
 #ifndef QEC_PHASE_STATS
 #define QEC_PHASE_STATS 0
 #endif
+//   QEC_ABLATE       timing experiments only (wrong outputs): 1 = skip the post-processing
+#ifndef QEC_ABLATE
+#define QEC_ABLATE 0
+#endif
 #define QEC_PICK(macro, dflt) ((macro) >= 0 ? (macro) != 0 : (dflt))
 
 // Per-variant tuning: minimum waves per SIMD for the register allocator, and the options above.
@@ -383,11 +387,14 @@ __device__ __forceinline__ void check_pass_hard(float (&msg)[R][L], uint32_t sbi
 // Returns the hard-decision mask (bit l) of the new messages when HD is set.
 // hard: in = every incoming (check->variable) message is exactly +0 or 1.0; out = so is every
 // outgoing one (only tracked when the hard-message paths are enabled for this launch).
+// vagree (out, meaningful when hard comes out set): every variable's R outgoing messages are
+// equal (on every live lane), i.e. the new state passes var_pass_agree's test as it stands.
 template <int R, int L, int SEC, bool LAST, bool HD, class SH, class TU>
 __device__ __forceinline__ uint32_t var_pass(const BpArgs& a, float (&msg)[R][L], const Lane& ln, float pp,
-                                             float one_minus_pp, bool& hard)
+                                             float one_minus_pp, bool& hard, bool& vagree)
 {
     const bool hard_in = hard;
+    bool vsame = true;  // this lane's variables: all R outputs equal (float compare: NaN is unequal)
     uint32_t soft_bits = 0;  // OR of bits(q - q*q) over outputs not known to be hard: 0 iff all are 0 or 1
     // the short division's guard assumes every message is a probability in [0, 1], which
     // holds by induction when p' is (DecoderCPU.h:135-229); other p' always take the full path
@@ -493,6 +500,8 @@ __device__ __forceinline__ uint32_t var_pass(const BpArgs& a, float (&msg)[R][L]
             if (!zero) {
 #pragma unroll
                 for (int j = 0; j < ND; ++j) soft_bits |= __float_as_uint(__builtin_fmaf(-qd[j], qd[j], qd[j]));
+#pragma unroll
+                for (int j = 1; j < ND; ++j) vsame &= qd[j] == qd[0];
             }
         }
 #pragma unroll
@@ -510,7 +519,10 @@ __device__ __forceinline__ uint32_t var_pass(const BpArgs& a, float (&msg)[R][L]
             msg[r][l] = rot<SH>(qv[r], ln, sh == 0 ? 0 : P - sh);
         }
     }
-    if constexpr (TU::kSaturate) hard = (a.hardPaths & QEC_HP_FORMS) && hard_ok(pp) && all_live(soft_bits == 0u, ln.live);
+    if constexpr (TU::kSaturate) {
+        hard = (a.hardPaths & QEC_HP_FORMS) && hard_ok(pp) && all_live(soft_bits == 0u, ln.live);
+        vagree = hard && all_live(vsame, ln.live);
+    }
     return hdmask;
 }
 
@@ -576,9 +588,11 @@ __device__ __forceinline__ bool lane_syndrome_ok(const BpArgs& a, uint32_t hdmas
 // hard: every variable->check message of this sector is exactly +0 or 1.0 (wave-uniform).
 // agreed: set when the iteration took the agreement path (hard sector, every variable's inputs
 // equal), i.e. it mapped msg to check_pass_hard(msg) (wave-uniform).
+// vagree: the new state is hard and each variable's R messages are equal (set on the agreement
+// path, where the new state passed that test; tracked by var_pass otherwise).
 template <int R, int L, int SEC, int STOP, bool LAST, class SH, class TU>
 __device__ __forceinline__ bool iteration(const BpArgs& a, float (&msg)[R][L], uint32_t sbits, int n, Lane& ln,
-                                          float pp, float one_minus_pp, bool& hard, bool& agreed)
+                                          float pp, float one_minus_pp, bool& hard, bool& agreed, bool& vagree)
 {
     const int P = SH::P(a);
     // launder the permute bases so their per-rotation selects are recomputed inside the
@@ -587,13 +601,17 @@ __device__ __forceinline__ bool iteration(const BpArgs& a, float (&msg)[R][L], u
     constexpr bool HD = STOP == QEC_STOP_SYNDROME;
     uint32_t hdmask = 0;
     agreed = false;
+    vagree = false;
     if (TU::kSaturate && hard) {
         check_pass_hard<R, L>(msg, sbits);  // outputs are hard too: hard stays set for the var pass
         agreed = QEC_AGREE && (LAST || R >= 2) && var_pass_agree<R, L, SEC, HD, SH>(a, msg, ln, hdmask);
-        if (!agreed) hdmask = var_pass<R, L, SEC, LAST, HD, SH, TU>(a, msg, ln, pp, one_minus_pp, hard);
+        if (agreed)
+            vagree = true;
+        else
+            hdmask = var_pass<R, L, SEC, LAST, HD, SH, TU>(a, msg, ln, pp, one_minus_pp, hard, vagree);
     } else {
         check_pass<R, L>(msg, sbits);
-        hdmask = var_pass<R, L, SEC, LAST, HD, SH, TU>(a, msg, ln, pp, one_minus_pp, hard);
+        hdmask = var_pass<R, L, SEC, LAST, HD, SH, TU>(a, msg, ln, pp, one_minus_pp, hard, vagree);
     }
     if constexpr (STOP == QEC_STOP_REF) {
         if (n % 10 == 0) return group_all(lane_converged<R, L>(msg), ln.gb, P);  // DecoderCPU.h:287-290
@@ -608,14 +626,18 @@ __device__ __forceinline__ bool iteration(const BpArgs& a, float (&msg)[R][L], u
 // row r becomes q ^ c_r with c_r = s_r ^ XOR_l q[r][l] (on the bit patterns {0, 1.0f}).  Then
 //   L even: XOR_l F(q)[r][l] = XOR_l q[r][l], so c_r(F(q)) = c_r(q) and F(F(q)) = q;
 //   L odd:  c_r(F(q)) = 0, so F(F(q)) = F(q).
-// So once two consecutive iterations n-1, n take the agreement path (states S_n = F(S_{n-1}) and
-// S_{n+1} = F(S_n) both pass the agreement test), every later state is S_n or S_{n+1}: each passes
-// the test again, every later iteration (the last one, with the self message, included: see
-// var_pass_agree) is F again, and F^k(S_{n+1}) = F^(k mod 2)(S_{n+1}).  The stop tests repeat
-// too: the syndrome rule tested both states already (and did not stop); the reference rule's
-// convergence test holds on every hard state, so it stops at the next n' with n' % 10 == 0.
-// The sector therefore jumps straight to its last executed iteration: same registers, same
-// iteration count, same flags as running the iterations one by one (bit-identical).
+// Call a state "agreeing" if it is hard and every variable's R messages are equal -- exactly the
+// test var_pass_agree applies to F(q).  If the state S entering iteration n is agreeing and the
+// iteration takes the agreement path (F(S) is agreeing), every later state is F(S) or
+// F(F(S)) in {S, F(S)}: each is agreeing, so every later iteration (the last one, with the self
+// message, included: see var_pass_agree) is F again, and F^k(F(S)) = F^(k mod 2)(F(S)).  S is
+// known to be agreeing when it came from the agreement path, or from a var pass whose outputs
+// were all 0/1 and equal per variable (var_pass's vagree).  The stop tests repeat too: the
+// syndrome rule tested both states already (S when it was produced, F(S) now) and did not stop;
+// the reference rule's convergence test holds on every hard state, so it stops at the next
+// n' with n' % 10 == 0.  The sector therefore jumps straight to its last executed iteration:
+// same registers, same iteration count, same flags as running the iterations one by one
+// (bit-identical).
 template <int STOP>
 __device__ __forceinline__ int cycle_end(int n, int N)
 {
@@ -656,8 +678,12 @@ __device__ __forceinline__ void decode_sector(const BpArgs& a, Lane& ln, long lo
     bool active = in_range;  // group-uniform
     int it = 0;
     int n = 0;
-    int agree_run = 0;  // consecutive iterations that took the agreement path (wave-uniform)
-    bool agreed = false;
+    // in_agree: the state entering the next iteration is hard and every variable's R messages
+    // are equal (wave-uniform); st_agreed: this group's current state passed that test (it was
+    // produced by the agreement path or is one of a cycle's two states), so the post-processing
+    // can read it lane-locally
+    bool in_agree = false, st_agreed = false;
+    bool agreed = false, vagree = false;
     int ph_soft = 0, ph_hard = 0, ph_agree = 0, ph_jump = 0;  // QEC_PHASE_STATS
     // iterations 0 .. N-2 (DecoderCPU.h:280-291); the last one is peeled below
     for (; n < N - 1; ++n) {
@@ -665,12 +691,15 @@ __device__ __forceinline__ void decode_sector(const BpArgs& a, Lane& ln, long lo
         if (active) {
             ++it;
             const bool was_hard = hard;
-            if (iteration<R, L, SEC, STOP, false, SH, TU>(a, msg, sbits, n, ln, pp, one_minus_pp, hard, agreed))
+            if (iteration<R, L, SEC, STOP, false, SH, TU>(a, msg, sbits, n, ln, pp, one_minus_pp, hard, agreed,
+                                                          vagree))
                 active = false;
             if constexpr (QEC_PHASE_STATS) { ph_soft += !was_hard; ph_hard += was_hard && !agreed; ph_agree += agreed; }
             if constexpr (TU::kSaturate) {
-                agree_run = agreed ? agree_run + 1 : 0;
-                if (agree_run >= 2 && active && (a.hardPaths & QEC_HP_CYCLE)) {
+                st_agreed = vagree;
+                // cycle_end: the state entering this iteration passed the agreement test and this
+                // iteration took the agreement path
+                if (agreed && in_agree && active && (a.hardPaths & QEC_HP_CYCLE)) {
                     const int last = cycle_end<STOP>(n, N);
                     if ((last - n) & 1) check_pass_hard<R, L>(msg, sbits);
                     it += last - n;
@@ -678,33 +707,63 @@ __device__ __forceinline__ void decode_sector(const BpArgs& a, Lane& ln, long lo
                     active = false;
                     n = N;  // skips the peeled last iteration too
                 }
+                in_agree = vagree;
             }
         }
     }
     if (n == N - 1 && active) {
         ++it;
         const bool was_hard = hard;
-        iteration<R, L, SEC, STOP, true, SH, TU>(a, msg, sbits, n, ln, pp, one_minus_pp, hard, agreed);
+        iteration<R, L, SEC, STOP, true, SH, TU>(a, msg, sbits, n, ln, pp, one_minus_pp, hard, agreed, vagree);
         if constexpr (QEC_PHASE_STATS) { ph_soft += !was_hard; ph_hard += was_hard && !agreed; ph_agree += agreed; }
+        st_agreed = vagree;
     }
 
+    if constexpr (QEC_ABLATE == 1) {
+        iters_out = it + (int)__float_as_uint(msg[0][0]);
+        return;
+    }
     // ---- post-processing of Decode (DecoderCPU.h:354-384) ----
-    const bool conv = group_all(lane_converged<R, L>(msg), gb, P);
     uint8_t* __restrict__ e = SEC ? a.eZ : a.eX;
     const int* et = SH::template table<SEC>(a);
-    uint32_t hdmask = 0;
+    bool conv, syn_ok;
+    if (TU::kSaturate && all_live(st_agreed, in_range)) {
+        // Every live group's state is hard and each variable's R messages are equal: the hard
+        // decision is the value on any one of its edges (row 0's, rotation S[0][l], 0 with the
+        // relabelling), the syndrome of that decision on check (r, i) is the XOR of the check's
+        // own L messages (each equals its variable's decision), and every message is outside
+        // (0.01, 0.99).  Same outputs as the general path below, without its 2 R L rotations.
 #pragma unroll
-    for (int l = 0; l < L; ++l) {
-        bool hd = false;  // e[v] = any edge message >= 0.5f (DecoderCPU.h:354-373)
+        for (int l = 0; l < L; ++l) {
+            const bool hd = rot<SH>(msg[0][l], ln, SH::template shift<SEC, L>(et, 0, l)) >= 0.5f;
+            if (in_range) e[b * (long long)a.n + l * P + wrap(i + SH::template coloff<SEC>(a, l), P)] = (uint8_t)hd;
+        }
+        bool match = true;
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-            const int sh = SH::template shift<SEC, L>(et, r, l);
-            hd |= rot<SH>(msg[r][l], ln, sh) >= 0.5f;
+            uint32_t x = 0;
+#pragma unroll
+            for (int l = 0; l < L; ++l) x ^= __float_as_uint(msg[r][l]);
+            match &= (x != 0u) == (((sbits >> r) & 1u) != 0u);
         }
-        hdmask |= (uint32_t)hd << l;
-        if (in_range) e[b * (long long)a.n + l * P + wrap(i + SH::template coloff<SEC>(a, l), P)] = (uint8_t)hd;
+        conv = true;
+        syn_ok = group_all(match, gb, P);
+    } else {
+        conv = group_all(lane_converged<R, L>(msg), gb, P);
+        uint32_t hdmask = 0;
+#pragma unroll
+        for (int l = 0; l < L; ++l) {
+            bool hd = false;  // e[v] = any edge message >= 0.5f (DecoderCPU.h:354-373)
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const int sh = SH::template shift<SEC, L>(et, r, l);
+                hd |= rot<SH>(msg[r][l], ln, sh) >= 0.5f;
+            }
+            hdmask |= (uint32_t)hd << l;
+            if (in_range) e[b * (long long)a.n + l * P + wrap(i + SH::template coloff<SEC>(a, l), P)] = (uint8_t)hd;
+        }
+        syn_ok = group_all(lane_syndrome_ok<R, L, SEC, SH>(a, hdmask, sbits, ln), gb, P);
     }
-    const bool syn_ok = group_all(lane_syndrome_ok<R, L, SEC, SH>(a, hdmask, sbits, ln), gb, P);
 
     if (!syn_ok) flags |= SEC ? QEC_SYNDROME_FAIL_Z : QEC_SYNDROME_FAIL_X;
     if (!conv) flags |= SEC ? QEC_CONVERGENCE_FAIL_Z : QEC_CONVERGENCE_FAIL_X;

@@ -40,21 +40,22 @@
 
 namespace qec {
 
-// Design options.  Each kernel variant carries its own measured choice of the first three
-// (Tune<> in the variant table below); defining one of those macros to 0 or 1 overrides it
-// for every variant.  The rest are global experiment switches.  tools/kbench sweeps them.
+// Design options.  Each kernel variant carries its own measured choice of RELABEL, MASK_SELECT,
+// PIPELINE, FASTDIV, ZEROSKIP and SATURATE (Tune<> in the variant table below); defining one of
+// those macros overrides it for every variant.  The rest are global experiment switches.
+// tools/kbench sweeps them.
 //   QEC_RELABEL      spanning-tree lane relabelling (fewer ds_bpermute, but more distinct shifts)
 //   QEC_MASK_SELECT  rotation base chosen by a constant lane mask instead of hoisted addresses
 #ifndef QEC_RELABEL
 #define QEC_RELABEL -1
 #endif
 #ifndef QEC_MASK_SELECT
-#define QEC_MASK_SELECT 0
+#define QEC_MASK_SELECT -1
 #endif
 //   QEC_PIPELINE     1: issue column l+1's gathers before column l's arithmetic; 2: and pin
 //                    that order with a scheduling barrier
 #ifndef QEC_PIPELINE
-#define QEC_PIPELINE 0
+#define QEC_PIPELINE -1
 #endif
 //   QEC_FASTDIV      guarded short division (see div_short below)
 #ifndef QEC_FASTDIV
@@ -86,9 +87,12 @@ namespace qec {
 #define QEC_PICK(macro, dflt) ((macro) >= 0 ? (macro) != 0 : (dflt))
 
 // Per-variant tuning: minimum waves per SIMD for the register allocator, and the options above.
-template <int MINW_, bool RELABEL_, bool ZEROSKIP_, bool FASTDIV_, bool SATURATE_ = false, bool SPLIT_ = false>
+template <int MINW_, bool RELABEL_, bool ZEROSKIP_, bool FASTDIV_, bool SATURATE_ = false, bool SPLIT_ = false,
+          bool MASKSEL_ = false, int PIPE_ = 0>
 struct Tune {
     static constexpr int kMinWaves = MINW_;
+    static constexpr bool kMaskSelect = QEC_PICK(QEC_MASK_SELECT, MASKSEL_);
+    static constexpr int kPipeline = QEC_PIPELINE >= 0 ? QEC_PIPELINE : PIPE_;
     static constexpr bool kSplit = SPLIT_;  // QEC_OPT_SECTOR_SPLIT = 1 (auto) splits sectors for this variant
     static constexpr bool kRelabel = QEC_PICK(QEC_RELABEL, RELABEL_);
     static constexpr bool kZeroSkip = QEC_PICK(QEC_ZEROSKIP, ZEROSKIP_);
@@ -156,6 +160,7 @@ inline void relabel(const int* E, int R, int L, int P, bool on, int* S, int* D, 
 // live registers.
 struct RuntimeShifts {
     static constexpr bool kStatic = false;
+    static constexpr bool kMaskSelect = false;
     static constexpr int kP = 0;
     __device__ static int P(const BpArgs& a) { return a.P; }
     template <int SEC>
@@ -176,9 +181,10 @@ struct RuntimeShifts {
 // Compile-time: exponent tables produced by the QC_LDPC_CSS generator formula
 // (QEC_LDPC/QEC_LDPC_CSS.cu:37-90) evaluated by the compiler, so every rotation
 // address is a loop-invariant constant of the lane index.
-template <int J_, int K_, int L_, int P_, int S_, int T_, bool RL_>
+template <int J_, int K_, int L_, int P_, int S_, int T_, bool RL_, bool MS_ = false>
 struct GeneratedShifts {
     static constexpr bool kStatic = true;
+    static constexpr bool kMaskSelect = MS_;  // rotation base by constant lane mask (see rot_addr)
     static constexpr int kP = P_;
     struct Tables {
         int EX[J_][L_];
@@ -269,7 +275,7 @@ template <class SH>
 __device__ __forceinline__ int rot_addr(const Lane& ln, int s)
 {
     int base;
-    if constexpr (SH::kStatic && QEC_MASK_SELECT)
+    if constexpr (SH::kStatic && SH::kMaskSelect)
         base = select_lanes(ln.b0, ln.b1, lanes_below<SH::kP>(s));
     else
         base = (ln.i < s) ? ln.b1 : ln.b0;  // loop-invariant per s: hoisted by the compiler
@@ -405,14 +411,14 @@ __device__ __forceinline__ uint32_t var_pass(const BpArgs& a, float (&msg)[R][L]
     // QEC_PIPELINE: the gathers of column l + 1 are issued before column l is computed, so
     // their ds_bpermute latency hides behind column l's arithmetic in the same wave.
     float gnext[R];
-    if constexpr (QEC_PIPELINE) {
+    if constexpr (TU::kPipeline) {
 #pragma unroll
         for (int r = 0; r < R; ++r) gnext[r] = rot<SH>(msg[r][0], ln, SH::template shift<SEC, L>(et, r, 0));
     }
 #pragma unroll
     for (int l = 0; l < L; ++l) {
         float gv[R], bv[R], qv[R];
-        if constexpr (QEC_PIPELINE) {
+        if constexpr (TU::kPipeline) {
 #pragma unroll
             for (int r = 0; r < R; ++r) gv[r] = gnext[r];
             if (l + 1 < L) {
@@ -420,7 +426,7 @@ __device__ __forceinline__ uint32_t var_pass(const BpArgs& a, float (&msg)[R][L]
                 for (int r = 0; r < R; ++r)
                     gnext[r] = rot<SH>(msg[r][l + 1], ln, SH::template shift<SEC, L>(et, r, l + 1));
             }
-            if constexpr (QEC_PIPELINE >= 2) __builtin_amdgcn_sched_barrier(0);
+            if constexpr (TU::kPipeline >= 2) __builtin_amdgcn_sched_barrier(0);
         } else {
 #pragma unroll
             for (int r = 0; r < R; ++r) gv[r] = rot<SH>(msg[r][l], ln, SH::template shift<SEC, L>(et, r, l));
@@ -597,7 +603,7 @@ __device__ __forceinline__ bool iteration(const BpArgs& a, float (&msg)[R][L], u
     const int P = SH::P(a);
     // launder the permute bases so their per-rotation selects are recomputed inside the
     // loop instead of being hoisted into ~2 R L live registers
-    if constexpr (QEC_MASK_SELECT) asm volatile("" : "+v"(ln.b0), "+v"(ln.b1));
+    if constexpr (SH::kMaskSelect) asm volatile("" : "+v"(ln.b0), "+v"(ln.b1));
     constexpr bool HD = STOP == QEC_STOP_SYNDROME;
     uint32_t hdmask = 0;
     agreed = false;
@@ -870,7 +876,7 @@ static Variant rt()
 template <int J, int K, int L, int P, int S, int T, class TU>
 static Variant gen()
 {
-    return make_variant<J, K, L, GeneratedShifts<J, K, L, P, S, T, TU::kRelabel>, TU, true>(
+    return make_variant<J, K, L, GeneratedShifts<J, K, L, P, S, T, TU::kRelabel, TU::kMaskSelect>, TU, true>(
         P, S, T, "wave-circulant generated-shift");
 }
 
@@ -878,10 +884,14 @@ static Variant gen()
 // short division 7.11 ms vs 9.46 ms without them; P7 (9 syndromes per wave, so whole-wave
 // zero columns are rare) keeps 8 waves and only the short division.  The hard-message paths:
 // P61 @ p=0.01 6.24 vs 7.28 ms, @ p=0.05 7.22 vs 9.36 ms; P7 0.186 vs 0.199 ms (session-3 kbench).
+// With the hard paths and cycle jump the zero-skip test no longer pays for P61 (0.976 vs 0.987 ms
+// @ p=0.01, 2.45 vs 2.81 ms @ p=0.05; session-5 kbench, profiles/r01/session5/cmp_s5m_*.txt),
+// and once the hoisted rotation bases spill, selecting them by lane mask wins (P61 0.855 vs
+// 0.963 ms, cmp_s5o/s5p); P7 now prefers the full division (0.090 vs 0.093 ms).
 static const Variant kVariants[] = {
     // specialised: the two code files the reference ships
-    gen<4, 5, 10, 61, 9, 49, Tune<4, true, true, true, true>>(),
-    gen<3, 3, 6, 7, 2, 3, Tune<8, false, false, true, true, true>>(),
+    gen<4, 5, 10, 61, 9, 49, Tune<4, true, false, true, true, false, true, 1>>(),
+    gen<3, 3, 6, 7, 2, 3, Tune<8, false, false, false, true, true>>(),
 #ifndef QEC_KBENCH_MINIMAL  // experiment builds (tools/kbench) only compile the shipped-code kernels
     // runtime shifts, any P <= 64 with these block shapes
     rt<4, 5, 10>(),

@@ -929,19 +929,26 @@ const void* select_variant(const Code& c, std::string& name)
     return nullptr;
 }
 
+// QEC_OPT_SECTOR_SPLIT: 0 off, 1 the variant's tuned choice, 2 on (runtime-shift variants have
+// no split kernels: one wave per syndrome)
+bool decode_uses_split(const void* variant, int stop, int split)
+{
+    const Variant* v = static_cast<const Variant*>(variant);
+    return (split == 2 || (split == 1 && v->split_auto)) && v->split[stop] != nullptr;
+}
+
 int launch_decode(const void* variant, const Code& c, const uint8_t* sX, const uint8_t* sZ, long long B,
                   float errorProbability, int maxIter, int stop, uint8_t* eX, uint8_t* eZ, uint8_t* flags,
-                  int32_t* iters, float* q, int hardPaths, const int32_t* perm, int split, hipStream_t stream)
+                  int32_t* iters, float* q, int hardPaths, const int32_t* perm, int split, bool flags_zeroed,
+                  hipStream_t stream)
 {
     const Variant* v = static_cast<const Variant*>(variant);
     if (B <= 0) return QEC_OK;
     BpArgs a{};
     a.sX = sX; a.sZ = sZ; a.eX = eX; a.eZ = eZ; a.flags = flags; a.iters = iters; a.q = q;
     a.perm = perm;
-    // QEC_OPT_SECTOR_SPLIT: 0 off, 1 the variant's tuned choice, 2 on (runtime-shift variants
-    // have no split kernels: one wave per syndrome)
-    split = (split == 2 || (split == 1 && v->split_auto)) && v->split[stop] != nullptr;
-    if (split && hipMemsetAsync(flags, 0, (size_t)B, stream) != hipSuccess)
+    split = decode_uses_split(variant, stop, split);
+    if (split && !flags_zeroed && hipMemsetAsync(flags, 0, (size_t)B, stream) != hipSuccess)
         return fail(QEC_ERR_HIP, "bp_decode: flags memset failed");
     a.B = B;
     a.P = c.P;

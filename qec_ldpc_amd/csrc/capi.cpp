@@ -16,11 +16,13 @@ const char* last_error_cstr();
 const void* select_variant(const Code& c, std::string& name);
 int launch_decode(const void* variant, const Code& c, const uint8_t* sX, const uint8_t* sZ, long long B,
                   float errorProbability, int maxIter, int stop, uint8_t* eX, uint8_t* eZ, uint8_t* flags,
-                  int32_t* iters, float* q, int hardPaths, const int32_t* perm, int split, hipStream_t stream);
+                  int32_t* iters, float* q, int hardPaths, const int32_t* perm, int split, bool flags_zeroed,
+                  hipStream_t stream);
 size_t schedule_workspace_bytes(long long B, int mX, int mZ);
 long long schedule_max_batch();
-int launch_schedule(const uint8_t* sX, const uint8_t* sZ, long long B, int mX, int mZ, void* ws, int32_t** perm_out,
-                    hipStream_t st);
+int launch_schedule(const uint8_t* sX, const uint8_t* sZ, long long B, int mX, int mZ, void* ws,
+                    uint8_t* zero_flags, int32_t** perm_out, hipStream_t st);
+bool decode_uses_split(const void* variant, int stop, int split);
 int launch_sample_depolarizing(uint64_t seed, uint64_t start, long long B, int n, float p, uint8_t* x, uint8_t* z,
                                hipStream_t st);
 int launch_errors_from_draws(const int32_t* idx, const uint8_t* type, long long B, int W, int n, uint8_t* x,
@@ -285,19 +287,23 @@ static int dispatch_decode(qec_decoder* d, const uint8_t* sX, const uint8_t* sZ,
         return launch_decode_sparse(d->sparse, sX, sZ, B, p, maxIter, stop, eX, eZ, flags, iters, q, st);
     const int hp = d->hard_paths ? (QEC_HP_FORMS | (d->cycle_jump ? QEC_HP_CYCLE : 0)) : 0;
     const int32_t* perm = nullptr;
+    bool zeroed = false;
     if (B > 1 && B <= schedule_max_batch() && (d->schedule == 2 || (d->schedule == 1 && B >= kScheduleMinBatch))) {
         try {
             d->sched.reserve(schedule_workspace_bytes(B, d->code->mX, d->code->mZ));
         } catch (const std::exception& ex) {
             return fail(QEC_ERR_NOMEM, std::string("decode: dispatch-order workspace: ") + ex.what());
         }
+        // a sector-split launch ORs its flags into a zeroed array: the order pass zeroes it
+        zeroed = decode_uses_split(d->variant, stop, d->sector_split);
         int32_t* pm = nullptr;
-        const int rc = launch_schedule(sX, sZ, B, d->code->mX, d->code->mZ, d->sched.data(), &pm, st);
+        const int rc = launch_schedule(sX, sZ, B, d->code->mX, d->code->mZ, d->sched.data(), zeroed ? flags : nullptr,
+                                       &pm, st);
         if (rc) return rc;
         perm = pm;
     }
     return launch_decode(d->variant, *d->code, sX, sZ, B, p, maxIter, stop, eX, eZ, flags, iters, q, hp, perm,
-                         d->sector_split, st);
+                         d->sector_split, zeroed, st);
 }
 
 static const int32_t* syndrome_table(const qec_decoder* d)

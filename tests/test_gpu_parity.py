@@ -239,15 +239,17 @@ def test_split_flags_unaligned_and_dirty(env, key):
     tX, tZ = torch.from_numpy(sX).to(dev), torch.from_numpy(sZ).to(dev)
     eX = torch.empty((B, code.n), dtype=torch.uint8, device=dev)
     eZ = torch.empty((B, code.n), dtype=torch.uint8, device=dev)
-    for off in (0, 1, 2, 3):
+    for off, sched in ((0, 0), (1, 0), (2, 0), (3, 0), (1, 2), (2, 2)):  # schedule 2: the order pass zeroes flags
         buf = torch.full((B + 8,), 0xA5, dtype=torch.uint8, device=dev)
         fl = buf[off:off + B]
         dec.set_option("sector_split", 2)
+        dec.set_option("schedule", sched)
         try:
             dec.decode_batch_dev(tX, tZ, 0.05, 20, "fixed", eX, eZ, fl)
             torch.cuda.synchronize()
         finally:
             dec.set_option("sector_split", 1)
+            dec.set_option("schedule", 1)
         h = buf.cpu().numpy()
         assert np.array_equal(h[off:off + B], ref[2]), "offset %d" % off
         assert (h[:off] == 0xA5).all() and (h[off + B:] == 0xA5).all(), "offset %d: neighbours changed" % off
@@ -271,3 +273,30 @@ def test_schedule_many_chunks_identical(env, key):
             dec.set_option("schedule", 1)
     for a, b in zip(outs[0][:4], outs[1][:4]):
         assert np.array_equal(a, b)
+
+
+def test_schedule_workspace_across_calls(env):
+    """The dispatch-order counters live in the decoder's workspace and are re-zeroed by the
+    launches themselves (double-buffered by call parity): many ordered calls in a row, with
+    the batch size changing (and the workspace growing) between them, each decode to the same
+    bits as batch order."""
+    code, dec, _ = env["P61"]
+    x, z = depolarizing_errors(code.n, 31, 9000, 0.02)
+    sX, sZ = code.syndrome(0, x), code.syndrome(1, z)
+    ref = {}
+    dec.set_option("schedule", 0)
+    try:
+        for B in (5000, 9000, 4097):
+            ref[B] = dec.decode_batch(sX[:B], sZ[:B], 0.02, 12, "fixed", want_iters=True)
+    finally:
+        dec.set_option("schedule", 1)
+    dec.set_option("schedule", 2)
+    try:
+        for B in (5000, 9000, 4097, 5000, 9000, 9000, 4097, 2, 5000):
+            if B not in ref:
+                continue
+            got = dec.decode_batch(sX[:B], sZ[:B], 0.02, 12, "fixed", want_iters=True)
+            for a, b in zip(got[:4], ref[B][:4]):
+                assert np.array_equal(a, b), "B=%d" % B
+    finally:
+        dec.set_option("schedule", 1)

@@ -84,6 +84,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--hard-paths", type=int, default=1, help="QEC_OPT_HARD_PATHS for the timed run")
+    ap.add_argument("--no-gather", action="store_true",
+                    help="N > 1: skip the (untimed-step) RCCL gather of bit-packed decisions to rank 0")
     ap.add_argument("--no-full-arith", action="store_true",
                     help="skip the full_arithmetic re-timing (profiling runs: keeps the launch average clean)")
     args = ap.parse_args()
@@ -98,7 +100,10 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
-        dist.init_process_group("nccl" if torch.cuda.is_available() else "gloo")
+        # RCCL ("nccl") over xGMI; QEC_BENCH_BACKEND=gloo rehearses the multi-rank path with
+        # several ranks sharing one GPU (RCCL needs one GPU per rank)
+        dist.init_process_group(os.environ.get("QEC_BENCH_BACKEND") or "nccl")
+    local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
@@ -217,6 +222,9 @@ def main():
         hist = np.bincount(it_np.ravel(), minlength=iters + 1)
         out["iteration_histogram"] = {str(k): int(v) for k, v in enumerate(hist) if v}
 
+    if world > 1 and not args.no_gather:
+        out["gather"] = gather_step(dec, eX, eZ, fl, B, world, rank, dev, stream)
+
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(code, fname, sX.cpu().numpy(), sZ.cpu().numpy(), p, iters, args, eX, eZ, fl)
     if world > 1:
@@ -224,6 +232,39 @@ def main():
         dist.destroy_process_group()
     if rank == 0:
         print(json.dumps(out), flush=True)
+
+
+def gather_step(dec, eX, eZ, fl, B, world, rank, dev, stream):
+    """every rank bit-packs its decoded shard on the device and the records
+    are gathered to rank 0 over RCCL.  Measured after (not inside) the timed decode steps:
+    the decode itself needs no exchange."""
+    import torch
+    import torch.distributed as dist
+    from qec_ldpc_amd.gather import gather_records
+    rec = torch.empty((B, dec.record_bytes()), dtype=torch.uint8, device=dev)
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record(stream)
+    dec.pack_decisions_dev(eX, eZ, fl, rec, stream=stream)
+    b.record(stream)
+    torch.cuda.synchronize(dev)
+    pack_ms = a.elapsed_time(b)
+    gather_records(rec)  # warm-up (communicator set-up)
+    torch.cuda.synchronize(dev)
+    dist.barrier()
+    t0 = time.perf_counter()
+    full = gather_records(rec)
+    torch.cuda.synchronize(dev)
+    dist.barrier()
+    ms = (time.perf_counter() - t0) * 1e3
+    t = torch.tensor([ms, pack_ms], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    ok = True
+    if rank == 0:
+        ok = bool(torch.equal(full[:B], rec))
+    nbytes = B * rec.shape[1]
+    return {"record_bytes": int(rec.shape[1]), "bytes_per_rank": int(nbytes), "pack_ms": round(float(t[1]), 4),
+            "gather_ms": round(float(t[0]), 4), "root_GBps": round(world * nbytes / (float(t[0]) * 1e-3) / 1e9, 2),
+            "rank0_shard_intact": ok}
 
 
 def full_arithmetic(dec, step, stream, B, outs, reps=3, option="hard_paths"):

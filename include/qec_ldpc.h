@@ -208,6 +208,12 @@ int qec_syndrome_dev(qec_decoder* dec, const uint8_t* x, const uint8_t* z, size_
  * the device array counters[QEC_MC_NCOUNTERS] (uint64). */
 int qec_statistics_dev(qec_decoder* dec, const uint8_t* x, const uint8_t* z, const uint8_t* eX, const uint8_t* eZ,
                        const uint8_t* flags, size_t B, uint64_t* counters, void* stream);
+/* Decision records for gathering a sharded batch to one rank (the decoded
+ * vectors travel bit-packed): out is B x (2 ceil(n/8) + 1) bytes, per syndrome eX packed
+ * (bit j of byte k = qubit 8k + j), then eZ packed, then the ErrorCode flags byte.  Device
+ * buffers, enqueued on `stream`. */
+int qec_pack_decisions_dev(qec_decoder* dec, const uint8_t* eX, const uint8_t* eZ, const uint8_t* flags, size_t B,
+                           uint8_t* out, void* stream);
 /* A whole Monte-Carlo run on the device: `count` depolarising samples from `start` of stream
  * `seed`, in batches of `batch`: sample -> syndrome -> decode (stop rule `stop`) -> statistics.
  * Synchronous; fills *out. */

@@ -37,7 +37,8 @@ EXPORTS = (
     "qec_decoder_set_option", "qec_decoder_get_option",
     "qec_decode_batch", "qec_decode_batch_dev",
     "qec_sample_fixed_weight", "qec_get_statistics",
-    "qec_sample_depolarizing_dev", "qec_syndrome_dev", "qec_statistics_dev", "qec_monte_carlo",
+    "qec_sample_depolarizing_dev", "qec_syndrome_dev", "qec_statistics_dev", "qec_pack_decisions_dev",
+    "qec_monte_carlo",
 )
 MC_COUNTERS = ("withX", "withZ", "synX", "synZ", "logical", "corrected", "convX", "convZ")
 
@@ -106,6 +107,7 @@ def lib():
             "qec_sample_depolarizing_dev": (i, [vp, ctypes.c_uint64, ctypes.c_uint64, sz, f, vp, vp, vp]),
             "qec_syndrome_dev": (i, [vp, vp, vp, sz, vp, vp, vp]),
             "qec_statistics_dev": (i, [vp, vp, vp, vp, vp, vp, sz, vp, vp]),
+            "qec_pack_decisions_dev": (i, [vp, vp, vp, vp, sz, vp, vp]),
             "qec_monte_carlo": (i, [vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, f, i, i, sz,
                                     ctypes.POINTER(MCResult)]),
         }
@@ -333,6 +335,16 @@ class DecoderGPU:
         _check(lib().qec_statistics_dev(self._h, x.data_ptr(), z.data_ptr(), eX.data_ptr(), eZ.data_ptr(),
                                         flags.data_ptr(), x.shape[0], counters.data_ptr(),
                                         ctypes.c_void_p(self._stream(stream))), "qec_statistics_dev")
+
+    def record_bytes(self):
+        """Bytes of one decision record (qec_pack_decisions_dev): 2 ceil(n/8) + 1."""
+        return 2 * ((self.code.n + 7) // 8) + 1
+
+    def pack_decisions_dev(self, eX, eZ, flags, out, stream=None):
+        """Bit-packs a decoded device batch into out [B, record_bytes()] (uint8 device tensor)."""
+        _check(lib().qec_pack_decisions_dev(self._h, eX.data_ptr(), eZ.data_ptr(), flags.data_ptr(), eX.shape[0],
+                                            out.data_ptr(), ctypes.c_void_p(self._stream(stream))),
+               "qec_pack_decisions_dev")
 
     def monte_carlo(self, seed, start, count, p, max_iter, stop="syndrome", batch=65536):
         """Device Monte-Carlo run (sample -> syndrome -> decode -> statistics); returns a dict."""

@@ -36,6 +36,8 @@ const int32_t* sparse_plan_chkvar(const void* plan);
 int launch_decode_sparse(void* plan, const uint8_t* sX, const uint8_t* sZ, long long B, float errorProbability,
                          int maxIter, int stop, uint8_t* eX, uint8_t* eZ, uint8_t* flags, int32_t* iters, float* q,
                          hipStream_t stream);
+int launch_pack_decisions(const uint8_t* eX, const uint8_t* eZ, const uint8_t* flags, long long B, int n, uint8_t* out,
+                          hipStream_t st);
 int launch_statistics(const Code& c, const uint64_t* imp_dev, const uint8_t* x, const uint8_t* z, const uint8_t* eX,
                       const uint8_t* eZ, const uint8_t* flags, long long B, unsigned long long* counters, hipStream_t st);
 }  // namespace qec
@@ -491,6 +493,15 @@ int qec_syndrome_dev(qec_decoder* d, const uint8_t* x, const uint8_t* z, size_t 
     if (!d || (B && (!x || !z || !sX || !sZ))) return fail(QEC_ERR_ARG, "qec_syndrome_dev: bad argument");
     QEC_HIP_CHECK(hipSetDevice(d->device));
     return launch_syndrome(*d->code, syndrome_table(d), x, z, (long long)B, sX, sZ, static_cast<hipStream_t>(stream));
+}
+
+int qec_pack_decisions_dev(qec_decoder* d, const uint8_t* eX, const uint8_t* eZ, const uint8_t* flags, size_t B,
+                           uint8_t* out, void* stream)
+{
+    if (!d || (B && (!eX || !eZ || !flags || !out))) return fail(QEC_ERR_ARG, "qec_pack_decisions_dev: bad argument");
+    if (B > (size_t)1 << 36) return fail(QEC_ERR_ARG, "qec_pack_decisions_dev: batch too large");
+    QEC_HIP_CHECK(hipSetDevice(d->device));
+    return launch_pack_decisions(eX, eZ, flags, (long long)B, d->code->n, out, static_cast<hipStream_t>(stream));
 }
 
 int qec_statistics_dev(qec_decoder* d, const uint8_t* x, const uint8_t* z, const uint8_t* eX, const uint8_t* eZ,

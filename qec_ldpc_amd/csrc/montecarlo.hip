@@ -193,6 +193,29 @@ __global__ __launch_bounds__(64 * kStatWaves) void statistics_kernel(
     if (threadIdx.x < C_N && part[threadIdx.x]) atomicAdd(&counters[threadIdx.x], part[threadIdx.x]);
 }
 
+// Decision records for the cross-rank gather: per syndrome, eX bit-packed
+// (ceil(n/8) bytes, bit j of byte k = qubit 8k + j), then eZ the same way, then the flags byte.
+// One thread per output byte; each reads its 8 (contiguous) decision bytes.
+__global__ void pack_decisions_kernel(const uint8_t* __restrict__ eX, const uint8_t* __restrict__ eZ,
+                                      const uint8_t* __restrict__ flags, long long B, int n,
+                                      uint8_t* __restrict__ out)
+{
+    const int nb = (n + 7) / 8, rec = 2 * nb + 1;
+    const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= B * rec) return;
+    const long long b = t / rec;
+    const int k = (int)(t - b * rec);
+    if (k == 2 * nb) {
+        out[t] = flags[b];
+        return;
+    }
+    const uint8_t* e = (k < nb ? eX : eZ) + b * n;
+    const int q0 = 8 * (k < nb ? k : k - nb);
+    uint32_t v = 0;
+    for (int j = 0; j < 8 && q0 + j < n; ++j) v |= (uint32_t)(e[q0 + j] & 1) << j;
+    out[t] = (uint8_t)v;
+}
+
 // ---- launchers --------------------------------------------------------------
 static int launch_check(const char* what)
 {
@@ -255,6 +278,16 @@ int launch_statistics(const Code& c, const uint64_t* imp_dev, const uint8_t* x, 
     hipLaunchKernelGGL(statistics_kernel, dim3((unsigned)((B + kStatWaves - 1) / kStatWaves)), dim3(64 * kStatWaves), 0, st,
                        x, z, eX, eZ, flags, B, c.n, imp_dev, nrows, c.imp_words, counters);
     return launch_check("statistics");
+}
+
+int launch_pack_decisions(const uint8_t* eX, const uint8_t* eZ, const uint8_t* flags, long long B, int n, uint8_t* out,
+                          hipStream_t st)
+{
+    if (B <= 0) return QEC_OK;
+    const long long total = B * (2 * ((n + 7) / 8) + 1);
+    hipLaunchKernelGGL(pack_decisions_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, eX, eZ, flags, B,
+                       n, out);
+    return launch_check("pack_decisions");
 }
 
 }  // namespace qec

@@ -107,3 +107,24 @@ def test_monte_carlo_shards_add_up(env):
     b = dec.monte_carlo(5, 2500, 3500, 0.03, 50, "syndrome", batch=777)
     for k in q.MC_COUNTERS + ("tested", "iterationsX", "iterationsZ"):
         assert whole[k] == a[k] + b[k], k
+
+
+@pytest.mark.parametrize("key", ["P7", "P61"])
+def test_pack_decisions_matches_host(env, key):
+    """qec_pack_decisions_dev (the gather payload) equals the host packing of
+    the same decoded batch, including the partial last byte (P7: n = 42)."""
+    from qec_ldpc_amd.gather import pack_records, unpack_records
+    code, dec, _ = env[key]
+    B = 777
+    rng = np.random.default_rng(8)
+    sX = (rng.random((B, code.numEqsX)) < 0.05).astype(np.uint8)
+    sZ = (rng.random((B, code.numEqsZ)) < 0.05).astype(np.uint8)
+    eX, eZ, fl, _, _ = dec.decode_batch(sX, sZ, 0.02, 20, "fixed")
+    tX, tZ, tf = (torch.from_numpy(a).to(DEV) for a in (eX, eZ, fl))
+    rec = dev_u8(B, dec.record_bytes())
+    dec.pack_decisions_dev(tX, tZ, tf, rec)
+    torch.cuda.synchronize()
+    got = rec.cpu().numpy()
+    assert np.array_equal(got, pack_records(eX, eZ, fl))
+    a, b, c = unpack_records(got, code.n)
+    assert np.array_equal(a, eX) and np.array_equal(b, eZ) and np.array_equal(c, fl)

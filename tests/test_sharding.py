@@ -79,3 +79,43 @@ def test_two_rank_gloo_matches_single_process(tmp_path, code_paths):
     assert np.array_equal(r["full"], ref)
     assert r["counters"].tolist() == [int(x.any(1).sum()), int(z.any(1).sum())]
     assert r["tmax"][0] == 2.0
+
+
+def _gather_worker(rank, world, port, out):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from qec_ldpc_amd.gather import gather_records
+    rec = torch.full((5, 13), rank + 1, dtype=torch.uint8)
+    rec[:, 0] = torch.arange(5, dtype=torch.uint8) + 10 * rank
+    full = gather_records(rec)
+    if rank == 0:
+        np.save(out, full.numpy())
+    else:
+        assert full is None
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gather_records_two_ranks(tmp_path):
+    """The decision gather (qec_ldpc_amd.gather): rank 0 receives every
+    rank's records in rank order."""
+    out = str(tmp_path / "g.npy")
+    mp.start_processes(_gather_worker, args=(2, _free_port(), out), nprocs=2, join=True, start_method="spawn")
+    full = np.load(out)
+    assert full.shape == (10, 13)
+    assert (full[:5, 1:] == 1).all() and (full[5:, 1:] == 2).all()
+    assert full[:, 0].tolist() == [0, 1, 2, 3, 4, 10, 11, 12, 13, 14]
+
+
+def test_pack_unpack_records_roundtrip():
+    from qec_ldpc_amd.gather import pack_records, unpack_records
+    rng = np.random.default_rng(3)
+    for n in (42, 610, 7, 8, 9):
+        eX = (rng.random((17, n)) < 0.3).astype(np.uint8)
+        eZ = (rng.random((17, n)) < 0.3).astype(np.uint8)
+        fl = rng.integers(0, 16, 17).astype(np.uint8)
+        rec = pack_records(eX, eZ, fl)
+        assert rec.shape == (17, 2 * ((n + 7) // 8) + 1)
+        a, b, c = unpack_records(rec, n)
+        assert np.array_equal(a, eX) and np.array_equal(b, eZ) and np.array_equal(c, fl)

@@ -654,22 +654,28 @@ __device__ __forceinline__ int cycle_end(int n, int N)
     return N - 1;
 }
 
-template <int R, int L, int SEC, int STOP, class SH, class TU>
-__device__ __forceinline__ void decode_sector(const BpArgs& a, Lane& ln, long long b, bool in_range, float pp,
-                                              uint32_t& flags, int& iters_out)
+// Syndrome bits of this lane's checks (r, i), r = 0..R-1, as bit r.
+template <int R, int SEC, class SH>
+__device__ __forceinline__ uint32_t load_sbits(const BpArgs& a, const Lane& ln, long long b, bool in_range)
 {
-    const int i = ln.i, gb = ln.gb;
     const int P = SH::P(a);
     const int m = R * P;
     const uint8_t* __restrict__ s = SEC ? a.sZ : a.sX;
-
-    // syndrome bits of checks (r, i)
     uint32_t sbits = 0;
     if (in_range) {
 #pragma unroll
         for (int r = 0; r < R; ++r)
-            sbits |= (uint32_t)(s[b * m + r * P + wrap(i + SH::template rowoff<SEC>(a, r), P)] & 1) << r;
+            sbits |= (uint32_t)(s[b * m + r * P + wrap(ln.i + SH::template rowoff<SEC>(a, r), P)] & 1) << r;
     }
+    return sbits;
+}
+
+template <int R, int L, int SEC, int STOP, class SH, class TU>
+__device__ __forceinline__ void decode_sector(const BpArgs& a, Lane& ln, long long b, bool in_range, float pp,
+                                              uint32_t sbits, uint32_t& flags, int& iters_out)
+{
+    const int i = ln.i, gb = ln.gb;
+    const int P = SH::P(a);
 
     // InitVarNodes: every edge starts at p' (DecoderCPU.h:135-148, 265-267)
     float msg[R][L];
@@ -792,13 +798,18 @@ __device__ __forceinline__ void decode_sector(const BpArgs& a, Lane& ln, long lo
 #ifndef QEC_MIN_WAVES_PER_EU
 #define QEC_MIN_WAVES_PER_EU 0  // 0: per-variant defaults below
 #endif
+#ifndef QEC_SYN_MINW_DELTA
+#define QEC_SYN_MINW_DELTA 0    // experiment: the syndrome-stop kernels' min waves per SIMD, relative
+#endif
 
 // MINW: minimum waves per SIMD the register allocator must allow (5 -> <= 96 VGPRs), measured
 // per variant with tools/kbench (P61: 5 waves beat 4 by 4 %; see profiles/).
 // SPLIT: waves 2k and 2k+1 decode sectors X and Z of group k (adjacent waves, one workgroup);
 // the launch zeroed flags[] and each sector ORs in its bits.  Otherwise one wave decodes both.
 template <int RX, int RZ, int L, int STOP, class SH, class TU, bool SPLIT>
-__global__ __launch_bounds__(64 * QEC_WAVES_PER_BLOCK, (QEC_MIN_WAVES_PER_EU ? QEC_MIN_WAVES_PER_EU : TU::kMinWaves))
+__global__ __launch_bounds__(64 * QEC_WAVES_PER_BLOCK,
+                             (QEC_MIN_WAVES_PER_EU ? QEC_MIN_WAVES_PER_EU : TU::kMinWaves) +
+                                 (STOP == QEC_STOP_SYNDROME ? QEC_SYN_MINW_DELTA : 0))
 void bp_decode_kernel(const BpArgs a)
 {
     const int lane = threadIdx.x & 63;
@@ -820,8 +831,15 @@ void bp_decode_kernel(const BpArgs a)
     int itX = 0, itZ = 0;
     Lane ln{i, gb, 4 * (gb + i), 4 * (gb + i + P), in_range};
     const bool doX = !SPLIT || (wave & 1) == 0;  // wave-uniform
-    if (doX) decode_sector<RX, L, 0, STOP, SH, TU>(a, ln, b, in_range, pp, flags, itX);
-    if (!doX || !SPLIT) decode_sector<RZ, L, 1, STOP, SH, TU>(a, ln, b, in_range, pp, flags, itZ);
+#ifndef QEC_PREFETCH_Z
+#define QEC_PREFETCH_Z 1
+#endif
+    // both sectors' syndrome loads are issued up front: the Z load's latency hides behind X
+    const uint32_t sbX = doX ? load_sbits<RX, 0, SH>(a, ln, b, in_range) : 0u;
+    uint32_t sbZ = (QEC_PREFETCH_Z && (!doX || !SPLIT)) ? load_sbits<RZ, 1, SH>(a, ln, b, in_range) : 0u;
+    if (doX) decode_sector<RX, L, 0, STOP, SH, TU>(a, ln, b, in_range, pp, sbX, flags, itX);
+    if (!QEC_PREFETCH_Z && (!doX || !SPLIT)) sbZ = load_sbits<RZ, 1, SH>(a, ln, b, in_range);
+    if (!doX || !SPLIT) decode_sector<RZ, L, 1, STOP, SH, TU>(a, ln, b, in_range, pp, sbZ, flags, itZ);
     if (in_range && i == 0) {
         if constexpr (!SPLIT) {
             a.flags[b] = (uint8_t)flags;

@@ -52,8 +52,7 @@ namespace qec {
 #ifndef QEC_MASK_SELECT
 #define QEC_MASK_SELECT -1
 #endif
-//   QEC_PIPELINE     1: issue column l+1's gathers before column l's arithmetic; 2: and pin
-//                    that order with a scheduling barrier
+//   QEC_PIPELINE     D: keep the gathers of the next D columns in flight during a column's arithmetic
 #ifndef QEC_PIPELINE
 #define QEC_PIPELINE -1
 #endif
@@ -408,25 +407,32 @@ __device__ __forceinline__ uint32_t var_pass(const BpArgs& a, float (&msg)[R][L]
     const int P = SH::P(a);
     const int* et = SH::template table<SEC>(a);
     uint32_t hdmask = 0;
-    // QEC_PIPELINE: the gathers of column l + 1 are issued before column l is computed, so
-    // their ds_bpermute latency hides behind column l's arithmetic in the same wave.
-    float gnext[R];
-    if constexpr (TU::kPipeline) {
+    // QEC_PIPELINE = D: the gathers of columns l + 1 .. l + D are in flight while column l is
+    // computed, so their ds_bpermute latency hides behind column l's arithmetic in the same wave
+    // (the per-column uniform branches below end basic blocks, so the compiler cannot do this).
+    constexpr int D = TU::kPipeline > 0 ? (TU::kPipeline < L ? TU::kPipeline : L - 1) : 0;
+    float gq[D > 0 ? D : 1][R];  // gq[k]: gathers of column l + 1 + k
+    if constexpr (D > 0) {
 #pragma unroll
-        for (int r = 0; r < R; ++r) gnext[r] = rot<SH>(msg[r][0], ln, SH::template shift<SEC, L>(et, r, 0));
+        for (int k = 0; k < D; ++k)
+#pragma unroll
+            for (int r = 0; r < R; ++r) gq[k][r] = rot<SH>(msg[r][k], ln, SH::template shift<SEC, L>(et, r, k));
     }
 #pragma unroll
     for (int l = 0; l < L; ++l) {
         float gv[R], bv[R], qv[R];
-        if constexpr (TU::kPipeline) {
+        if constexpr (D > 0) {
 #pragma unroll
-            for (int r = 0; r < R; ++r) gv[r] = gnext[r];
-            if (l + 1 < L) {
+            for (int r = 0; r < R; ++r) gv[r] = gq[0][r];
+#pragma unroll
+            for (int k = 0; k + 1 < D; ++k)
+#pragma unroll
+                for (int r = 0; r < R; ++r) gq[k][r] = gq[k + 1][r];
+            if (l + D < L) {
 #pragma unroll
                 for (int r = 0; r < R; ++r)
-                    gnext[r] = rot<SH>(msg[r][l + 1], ln, SH::template shift<SEC, L>(et, r, l + 1));
+                    gq[D - 1][r] = rot<SH>(msg[r][l + D], ln, SH::template shift<SEC, L>(et, r, l + D));
             }
-            if constexpr (TU::kPipeline >= 2) __builtin_amdgcn_sched_barrier(0);
         } else {
 #pragma unroll
             for (int r = 0; r < R; ++r) gv[r] = rot<SH>(msg[r][l], ln, SH::template shift<SEC, L>(et, r, l));

@@ -83,6 +83,10 @@ namespace qec {
 #ifndef QEC_ABLATE
 #define QEC_ABLATE 0
 #endif
+//   QEC_TRACK_FROM   first iteration whose var pass tests whether the sector became hard
+#ifndef QEC_TRACK_FROM
+#define QEC_TRACK_FROM 2
+#endif
 #define QEC_PICK(macro, dflt) ((macro) >= 0 ? (macro) != 0 : (dflt))
 
 // Per-variant tuning: minimum waves per SIMD for the register allocator, and the options above.
@@ -396,7 +400,7 @@ __device__ __forceinline__ void check_pass_hard(float (&msg)[R][L], uint32_t sbi
 // equal (on every live lane), i.e. the new state passes var_pass_agree's test as it stands.
 template <int R, int L, int SEC, bool LAST, bool HD, class SH, class TU>
 __device__ __forceinline__ uint32_t var_pass(const BpArgs& a, float (&msg)[R][L], const Lane& ln, float pp,
-                                             float one_minus_pp, bool& hard, bool& vagree)
+                                             float one_minus_pp, bool& hard, bool& vagree, bool track = true)
 {
     const bool hard_in = hard;
     bool vsame = true;  // this lane's variables: all R outputs equal (float compare: NaN is unequal)
@@ -509,7 +513,7 @@ __device__ __forceinline__ uint32_t var_pass(const BpArgs& a, float (&msg)[R][L]
             for (int j = 0; j < ND; ++j) qd[j] = num[j] / den[j];
         }
         if constexpr (TU::kSaturate) {
-            if (!zero) {
+            if (!zero && track) {
 #pragma unroll
                 for (int j = 0; j < ND; ++j) soft_bits |= __float_as_uint(__builtin_fmaf(-qd[j], qd[j], qd[j]));
 #pragma unroll
@@ -532,7 +536,7 @@ __device__ __forceinline__ uint32_t var_pass(const BpArgs& a, float (&msg)[R][L]
         }
     }
     if constexpr (TU::kSaturate) {
-        hard = (a.hardPaths & QEC_HP_FORMS) && hard_ok(pp) && all_live(soft_bits == 0u, ln.live);
+        hard = track && (a.hardPaths & QEC_HP_FORMS) && hard_ok(pp) && all_live(soft_bits == 0u, ln.live);
         vagree = hard && all_live(vsame, ln.live);
     }
     return hdmask;
@@ -623,7 +627,10 @@ __device__ __forceinline__ bool iteration(const BpArgs& a, float (&msg)[R][L], u
             hdmask = var_pass<R, L, SEC, LAST, HD, SH, TU>(a, msg, ln, pp, one_minus_pp, hard, vagree);
     } else {
         check_pass<R, L>(msg, sbits);
-        hdmask = var_pass<R, L, SEC, LAST, HD, SH, TU>(a, msg, ln, pp, one_minus_pp, hard, vagree);
+        // the hard-state test is skipped in the first QEC_TRACK_FROM iterations (they essentially
+        // never end hard; skipping only delays the exact hard forms, never changes a bit)
+        hdmask = var_pass<R, L, SEC, LAST, HD, SH, TU>(a, msg, ln, pp, one_minus_pp, hard, vagree,
+                                                       LAST || n >= QEC_TRACK_FROM);
     }
     if constexpr (STOP == QEC_STOP_REF) {
         if (n % 10 == 0) return group_all(lane_converged<R, L>(msg), ln.gb, P);  // DecoderCPU.h:287-290

@@ -83,6 +83,10 @@ namespace qec {
 #ifndef QEC_ABLATE
 #define QEC_ABLATE 0
 #endif
+//   QEC_TABLE0       iteration 0 from a per-workgroup table (iteration0)
+#ifndef QEC_TABLE0
+#define QEC_TABLE0 1
+#endif
 //   QEC_TRACK_FROM   first iteration whose var pass tests whether the sector became hard
 #ifndef QEC_TRACK_FROM
 #define QEC_TRACK_FROM 2
@@ -640,6 +644,76 @@ __device__ __forceinline__ bool iteration(const BpArgs& a, float (&msg)[R][L], u
     return false;
 }
 
+// ---- iteration 0 by table --------------------------------------------------------
+// Iteration 0 of BeliefPropogation starts from q = p' on every edge (DecoderCPU.h:265-267).  So
+// every factor of every check is a = 1 - 2p', every leave-one-out product is the same left fold
+// t = a^(L-1), and each check sends r0 = 0.5 (1 - t) or r1 = 0.5 (1 + t) on all its edges, chosen
+// by its syndrome bit.  A variable's R outputs then depend only on the R-bit pattern of its
+// checks' syndrome bits:  q0[pattern][j] = P1 / (P0 + P1),  P1 = p' prod_{k != j} r_{bit k},
+// P0 = (1 - p') prod_{k != j} (1 - r_{bit k}), ascending k (DecoderCPU.h:210-225).  The workgroup
+// builds that 2^R x R table once per sector with exactly the operations check_pass / var_pass
+// would run (so the same bits), and iteration 0 becomes gathers of syndrome bits and table reads.
+// Not used when iteration 0 is the last one (N = 1: the self message is included).
+template <int R, int L>
+__device__ __forceinline__ float table0_entry(float pp, int e)
+{
+    const float a = __builtin_fmaf(-2.0f, pp, 1.0f);  // 1.0f - 2.0f*q, as check_pass
+    float t = 1.0f;
+    if constexpr (L >= 2) {
+        t = a;  // 1.0f * a
+#pragma unroll
+        for (int k = 2; k < L; ++k) t = t * a;
+    }
+    const float r0 = __builtin_fmaf(-0.5f, t, 0.5f), r1 = __builtin_fmaf(0.5f, t, 0.5f);
+    const int idx = e / R, j = e - (e / R) * R;
+    float P0 = 1.0f - pp, P1 = pp;
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+        if (k == j) continue;
+        const float g = ((idx >> k) & 1) ? r1 : r0;
+        P0 = P0 * (1.0f - g);
+        P1 = P1 * g;
+    }
+    return P1 / (P0 + P1);
+}
+
+template <int R, int L, int SEC, int STOP, class SH>
+__device__ __forceinline__ bool iteration0(const BpArgs& a, float (&msg)[R][L], uint32_t sbits, const Lane& ln,
+                                           const float* __restrict__ tab)
+{
+    const int P = SH::P(a);
+    const int* et = SH::template table<SEC>(a);
+    constexpr bool HD = STOP == QEC_STOP_SYNDROME;
+    uint32_t hdmask = 0;
+#pragma unroll
+    for (int l = 0; l < L; ++l) {
+        int idx = 0;  // syndrome bits of this variable's R checks (var view, row r -> bit r)
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+            idx |= ((rot_i<SH>((int)sbits, ln, SH::template shift<SEC, L>(et, r, l)) >> r) & 1) << r;
+        float qv[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) qv[r] = tab[idx * R + r];
+        if constexpr (HD) {
+            bool hd = false;
+#pragma unroll
+            for (int r = 0; r < R; ++r) hd |= (qv[r] >= 0.5f);
+            hdmask |= (uint32_t)hd << l;
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int sh = SH::template shift<SEC, L>(et, r, l);
+            msg[r][l] = rot<SH>(qv[r], ln, sh == 0 ? 0 : P - sh);
+        }
+    }
+    if constexpr (STOP == QEC_STOP_REF) {
+        return group_all(lane_converged<R, L>(msg), ln.gb, P);  // n = 0: DecoderCPU.h:287-290
+    } else if constexpr (STOP == QEC_STOP_SYNDROME) {
+        return group_all(lane_syndrome_ok<R, L, SEC, SH>(a, hdmask, sbits, ln), ln.gb, P);
+    }
+    return false;
+}
+
 // ---- cycle jump --------------------------------------------------------------
 // On a hard sector the agreement path maps the check-view registers q to F(q) = check_pass_hard(q):
 // row r becomes q ^ c_r with c_r = s_r ^ XOR_l q[r][l] (on the bit patterns {0, 1.0f}).  Then
@@ -685,7 +759,8 @@ __device__ __forceinline__ uint32_t load_sbits(const BpArgs& a, const Lane& ln, 
 
 template <int R, int L, int SEC, int STOP, class SH, class TU>
 __device__ __forceinline__ void decode_sector(const BpArgs& a, Lane& ln, long long b, bool in_range, float pp,
-                                              uint32_t sbits, uint32_t& flags, int& iters_out)
+                                              uint32_t sbits, const float* __restrict__ tab0, uint32_t& flags,
+                                              int& iters_out)
 {
     const int i = ln.i, gb = ln.gb;
     const int P = SH::P(a);
@@ -710,7 +785,13 @@ __device__ __forceinline__ void decode_sector(const BpArgs& a, Lane& ln, long lo
     bool in_agree = false, st_agreed = false;
     bool agreed = false, vagree = false;
     int ph_soft = 0, ph_hard = 0, ph_agree = 0, ph_jump = 0;  // QEC_PHASE_STATS
-    // iterations 0 .. N-2 (DecoderCPU.h:280-291); the last one is peeled below
+    if (QEC_TABLE0 && N >= 2 && active) {  // iteration 0 by table (see iteration0)
+        ++it;
+        if (iteration0<R, L, SEC, STOP, SH>(a, msg, sbits, ln, tab0)) active = false;
+        if constexpr (QEC_PHASE_STATS) ph_soft += 1;
+        n = 1;
+    }
+    // iterations n .. N-2 (DecoderCPU.h:280-291); the last one is peeled below
     for (; n < N - 1; ++n) {
         if (!__any(active)) break;  // DecoderCPU.h:282 (fixed: only after a cycle jump)
         if (active) {
@@ -832,6 +913,15 @@ void bp_decode_kernel(const BpArgs a)
     const int g = lane / P;
     const int i = lane - g * P;
     const int gb = g * P;
+    // iteration-0 tables of both sectors (iteration0), built by the workgroup before any wave leaves
+    constexpr int kTabX = (1 << RX) * RX, kTabZ = (1 << RZ) * RZ;
+    __shared__ float tab0[QEC_TABLE0 ? kTabX + kTabZ : 1];
+    if constexpr (QEC_TABLE0) {
+        const float ppt = 2.0f / 3.0f * a.errorProbability;
+        for (int e = threadIdx.x; e < kTabX + kTabZ; e += blockDim.x)
+            tab0[e] = e < kTabX ? table0_entry<RX, L>(ppt, e) : table0_entry<RZ, L>(ppt, e - kTabX);
+        __syncthreads();
+    }
     const long long grp = SPLIT ? wave >> 1 : wave;
     const long long slot = grp * G + g;
     const bool in_range = (g < G) && (slot < a.B);
@@ -850,9 +940,9 @@ void bp_decode_kernel(const BpArgs a)
     // both sectors' syndrome loads are issued up front: the Z load's latency hides behind X
     const uint32_t sbX = doX ? load_sbits<RX, 0, SH>(a, ln, b, in_range) : 0u;
     uint32_t sbZ = (QEC_PREFETCH_Z && (!doX || !SPLIT)) ? load_sbits<RZ, 1, SH>(a, ln, b, in_range) : 0u;
-    if (doX) decode_sector<RX, L, 0, STOP, SH, TU>(a, ln, b, in_range, pp, sbX, flags, itX);
+    if (doX) decode_sector<RX, L, 0, STOP, SH, TU>(a, ln, b, in_range, pp, sbX, tab0, flags, itX);
     if (!QEC_PREFETCH_Z && (!doX || !SPLIT)) sbZ = load_sbits<RZ, 1, SH>(a, ln, b, in_range);
-    if (!doX || !SPLIT) decode_sector<RZ, L, 1, STOP, SH, TU>(a, ln, b, in_range, pp, sbZ, flags, itZ);
+    if (!doX || !SPLIT) decode_sector<RZ, L, 1, STOP, SH, TU>(a, ln, b, in_range, pp, sbZ, tab0 + kTabX, flags, itZ);
     if (in_range && i == 0) {
         if constexpr (!SPLIT) {
             a.flags[b] = (uint8_t)flags;

@@ -318,21 +318,24 @@ __device__ __forceinline__ bool outside(float x) { return !(x > 0.01f && x < 0.9
 //   q = div_fixup(q, d, n).
 // div_scale only rescales (by 2^64) when an operand or the quotient is near the ends of
 // the exponent range, and div_fixup only changes special cases (0, inf, NaN, over/underflow);
-// with d in [2^-98, 2], n = +0 or n in [2^-98, d] neither fires (no scaling, VCC = 0, so
-// div_fmas is a plain fma, and every residual fma is exact), so the same arithmetic without
-// them gives the same bits (8 instructions, measured 14.4 vs 24.7 SIMD-cycles).  The guard
-// below is evaluated for a whole column of divisions and the short path taken only when every
-// live lane of the wave passes it; otherwise the full sequence runs.
+// with d in [2^-98, 2] and n = +0 or n in [2^-98, d] neither fires.  On that domain the short
+// form below (6 instructions) is the correctly rounded quotient:
+//   y1 = fma(1 - d rcp(d), rcp(d), rcp(d)) is RN(1/d) -- checked for EVERY d in [2^-98, 2)
+//   (all significands, every exponent; d = 2 is exact) by tools/kbench/div_check.hip;
+//   q0 = RN(n y1) is then within one ulp of n/d, the residual fma(-d, q0, n) is exact, and
+//   by Markstein's theorem q1 = fma(r, y1, q0) = RN(n/d).  The same tool also compares it with
+//   the IEEE quotient on 8.6e9 random and near-midpoint pairs of the domain: no difference
+//   (profiles/r01/session5/div_check.json).
+// The guard below is evaluated for a whole column of divisions and the short path taken only
+// when every live lane of the wave passes it; otherwise the full sequence runs.
 __device__ __forceinline__ float div_short(float n, float d)
 {
-    float r = __builtin_amdgcn_rcpf(d);
-    const float e = __builtin_fmaf(-d, r, 1.0f);
-    r = __builtin_fmaf(e, r, r);
-    float q = n * r;
-    const float e2 = __builtin_fmaf(-d, q, n);
-    q = __builtin_fmaf(e2, r, q);
-    const float e3 = __builtin_fmaf(-d, q, n);
-    return __builtin_fmaf(e3, r, q);
+    const float y0 = __builtin_amdgcn_rcpf(d);
+    const float e = __builtin_fmaf(-d, y0, 1.0f);
+    const float y1 = __builtin_fmaf(e, y0, y0);
+    const float q0 = n * y1;
+    const float r = __builtin_fmaf(-d, q0, n);
+    return __builtin_fmaf(r, y1, q0);
 }
 // n = t1 >= 0 and d = t0 + t1 with t0, t1 products of probabilities in [0, 1] (so d <= 2):
 // short path valid iff d >= 2^-98 (a float compare: NaN fails) and n is +0 or >= 2^-98

@@ -60,6 +60,10 @@ namespace qec {
 #ifndef QEC_FASTDIV
 #define QEC_FASTDIV -1
 #endif
+//   QEC_GUARD_MIN    1: the short-division guard of a column as two min-reductions
+#ifndef QEC_GUARD_MIN
+#define QEC_GUARD_MIN 1
+#endif
 //   QEC_ZEROSKIP     a column whose every numerator is +0 (and denominator > 0) on every live
 //                    lane gets q = +0 without dividing (IEEE: +0 / d = +0 for d > 0)
 #ifndef QEC_ZEROSKIP
@@ -503,9 +507,24 @@ __device__ __forceinline__ uint32_t var_pass(const BpArgs& a, float (&msg)[R][L]
         }
         if constexpr (TU::kFastDiv) {
             if (!zero) {
+#if QEC_GUARD_MIN
+                // the guard of every division of the column at once, as unsigned minima of bit
+                // patterns (non-negative floats order like their bits): numerators minus 1 (+0
+                // wraps to the top), denominators as they are.  A NaN sorts above every number, so
+                // it never fails the guard; the short form then returns NaN, as the IEEE division
+                // does.
+                uint32_t nm = 0xFFFFFFFFu, dm = 0xFFFFFFFFu;
+#pragma unroll
+                for (int j = 0; j < ND; ++j) {
+                    nm = min(nm, __float_as_uint(num[j]) - 1u);
+                    dm = min(dm, __float_as_uint(den[j]));
+                }
+                const bool ok = (int)(dm >= __float_as_uint(0x1p-98f)) & (int)(nm >= __float_as_uint(0x1p-98f) - 1u);
+#else
                 bool ok = true;
 #pragma unroll
                 for (int j = 0; j < ND; ++j) ok &= div_short_ok(num[j], den[j]);
+#endif
                 fast = pp_ok && all_live(ok, ln.live);
             }
         }
@@ -1011,11 +1030,12 @@ static Variant gen()
 // With the hard paths and cycle jump the zero-skip test no longer pays for P61 (0.976 vs 0.987 ms
 // @ p=0.01, 2.45 vs 2.81 ms @ p=0.05; session-5 kbench, profiles/r01/session5/cmp_s5m_*.txt),
 // and once the hoisted rotation bases spill, selecting them by lane mask wins (P61 0.855 vs
-// 0.963 ms, cmp_s5o/s5p); P7 now prefers the full division (0.090 vs 0.093 ms).
+// 0.963 ms, cmp_s5o/s5p).  With the 6-instruction short division and the min-reduced guard P7
+// takes the short division again (0.090 vs 0.092 ms, cmp_s6j).
 static const Variant kVariants[] = {
     // specialised: the two code files the reference ships
     gen<4, 5, 10, 61, 9, 49, Tune<4, true, false, true, true, false, true, 1>>(),
-    gen<3, 3, 6, 7, 2, 3, Tune<8, false, false, false, true, true>>(),
+    gen<3, 3, 6, 7, 2, 3, Tune<8, false, false, true, true, true>>(),
 #ifndef QEC_KBENCH_MINIMAL  // experiment builds (tools/kbench) only compile the shipped-code kernels
     // runtime shifts, any P <= 64 with these block shapes
     rt<4, 5, 10>(),

@@ -15,16 +15,16 @@
 // index).  The order inside one (chunk, bucket) depends on LDS-atomic timing and is not
 // deterministic, which is harmless for the same reason.
 //
-// Counting sort over kBuckets weight buckets (integer/byte work, HBM/L2-bound) in three
+// Counting sort over kBuckets weight buckets (integer/byte work, HBM/L2-bound) in two
 // launches with no global atomics (same-address atomics from every workgroup serialise at L2):
 //   hist    : one workgroup per chunk of consecutive syndromes, four threads per syndrome
 //             (16-byte loads along a quarter of its rows, 8 in flight); the workgroup
 //             histograms the buckets in LDS and stores its counts [chunk][bucket]
-//   offsets : one workgroup; four threads per bucket sum a quarter of the chunks each, the
-//             bucket totals are scanned heaviest-first, and every (chunk, bucket) count is
-//             replaced by that chunk's first position in the bucket
-//   scatter : each chunk's workgroup places its syndromes from its own offsets (LDS atomics),
-//             perm[pos] = b
+//   scatter : each chunk's workgroup derives its own first position in every bucket from the
+//             whole count matrix (bucket totals scanned heaviest-first, plus the counts of the
+//             chunks before it) and places its syndromes (LDS atomics), perm[pos] = b.
+//             (A separate one-workgroup offsets launch was measured at 10.6 us of a 27.7 us
+//             P7 order pass, profiles/r01/session7/rocprof_p7_kernel_stats_s7a.csv.)
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -34,11 +34,8 @@
 namespace qec {
 
 constexpr int kBuckets = 256;    // bucket k = 255 - min(weight, 255): 0 = heaviest
-constexpr int kSchedThreads = 256;
 constexpr int kHistThreads = 1024;
 constexpr int kHistSplit = 4;    // threads per syndrome in the weight pass
-constexpr int kOffThreads = 1024;
-constexpr int kOffSplit = kOffThreads / kBuckets;  // threads per bucket in the offsets pass
 constexpr int kMaxChunks = 1024;
 constexpr int kMinChunk = 256;   // rows per chunk
 constexpr int kMaxChunk = 4096;
@@ -109,66 +106,61 @@ __global__ __launch_bounds__(kHistThreads) void schedule_hist_kernel(const uint8
     if (t < kBuckets) counts[(long long)blockIdx.x * kBuckets + t] = h[t];
 }
 
-// counts[c][k] -> position of chunk c's first syndrome of bucket k.  kOffSplit threads per
-// bucket, each over a contiguous range of chunks, loaded kOffBatch at a time into registers.
+// Scatter with the offsets computed in place: workgroup c needs, for every bucket k, the
+// total of every heavier bucket (all chunks) plus bucket k's count in chunks before c.  Its
+// kScatSplit threads per bucket each sum a contiguous quarter of the count matrix's rows
+// (coalesced 1 KiB rows, kOffBatch loads in flight), the quarters meet in LDS, and one
+// 256-wide scan turns the totals into bucket starts.  Every workgroup re-reads the whole
+// [chunks][256] matrix (256 KiB at 256 chunks, from L2), which costs less than a separate
+// single-workgroup offsets launch and its gap.  Then its syndromes are placed with LDS atomics.
+constexpr int kScatThreads = 1024;
+constexpr int kScatSplit = kScatThreads / kBuckets;
 constexpr int kOffBatch = 32;
-__global__ __launch_bounds__(kOffThreads) void schedule_offsets_kernel(uint32_t* __restrict__ counts, int nch)
+__global__ __launch_bounds__(kScatThreads) void schedule_scatter_kernel(const uint8_t* __restrict__ key, long long B,
+                                                                      int chunk, int nch,
+                                                                      const uint32_t* __restrict__ counts,
+                                                                      int32_t* __restrict__ perm)
 {
-    __shared__ uint32_t part[kOffSplit][kBuckets];
-    __shared__ uint32_t base[kBuckets];
-    const int k = threadIdx.x % kBuckets, q = threadIdx.x / kBuckets;
-    const int c0 = nch * q / kOffSplit, c1 = nch * (q + 1) / kOffSplit;
-    uint32_t sum = 0;
-    for (int cb = c0; cb < c1; cb += kOffBatch) {
-        uint32_t v[kOffBatch];
-#pragma unroll
-        for (int j = 0; j < kOffBatch; ++j) v[j] = cb + j < c1 ? counts[(cb + j) * kBuckets + k] : 0u;
-#pragma unroll
-        for (int j = 0; j < kOffBatch; ++j) sum += v[j];
-    }
-    part[q][k] = sum;
-    __syncthreads();
-    if (q == 0) {
-        uint32_t tot = 0;
-#pragma unroll
-        for (int j = 0; j < kOffSplit; ++j) tot += part[j][k];
-        base[k] = tot;
-    }
-    __syncthreads();
-    for (int o = 1; o < kBuckets; o <<= 1) {  // inclusive scan of the bucket totals
-        const uint32_t add = (q == 0 && k >= o) ? base[k - o] : 0u;
-        __syncthreads();
-        if (q == 0) base[k] += add;
-        __syncthreads();
-    }
-    uint32_t run = (k ? base[k - 1] : 0u);  // exclusive
-#pragma unroll
-    for (int j = 0; j < kOffSplit; ++j)
-        if (j < q) run += part[j][k];
-    for (int cb = c0; cb < c1; cb += kOffBatch) {
-        uint32_t v[kOffBatch];
-#pragma unroll
-        for (int j = 0; j < kOffBatch; ++j) v[j] = cb + j < c1 ? counts[(cb + j) * kBuckets + k] : 0u;
-#pragma unroll
-        for (int j = 0; j < kOffBatch; ++j) {
-            if (cb + j < c1) counts[(cb + j) * kBuckets + k] = run;
-            run += v[j];
-        }
-    }
-}
-
-__global__ __launch_bounds__(kSchedThreads) void schedule_scatter_kernel(const uint8_t* __restrict__ key, long long B,
-                                                                       int chunk,
-                                                                       const uint32_t* __restrict__ offsets,
-                                                                       int32_t* __restrict__ perm)
-{
+    __shared__ uint32_t before[kScatSplit][kBuckets];
+    __shared__ uint32_t total[kScatSplit][kBuckets];
     __shared__ uint32_t cur[kBuckets];
     const int t = threadIdx.x;
-    cur[t] = offsets[(long long)blockIdx.x * kBuckets + t];  // kSchedThreads == kBuckets
+    const int k = t % kBuckets, q = t / kBuckets;
+    const int c = blockIdx.x;
+    const int c0 = nch * q / kScatSplit, c1 = nch * (q + 1) / kScatSplit;
+    uint32_t pre = 0, all = 0;
+    for (int cb = c0; cb < c1; cb += kOffBatch) {
+        uint32_t v[kOffBatch];
+#pragma unroll
+        for (int j = 0; j < kOffBatch; ++j) v[j] = cb + j < c1 ? counts[(long long)(cb + j) * kBuckets + k] : 0u;
+#pragma unroll
+        for (int j = 0; j < kOffBatch; ++j) {
+            all += v[j];
+            pre += cb + j < c ? v[j] : 0u;
+        }
+    }
+    before[q][k] = pre;
+    total[q][k] = all;
     __syncthreads();
-    const long long r0 = (long long)blockIdx.x * chunk;
+    if (q == 0) {
+        uint32_t tot = 0, pb = 0;
+#pragma unroll
+        for (int j = 0; j < kScatSplit; ++j) { tot += total[j][k]; pb += before[j][k]; }
+        total[0][k] = tot;
+        before[0][k] = pb;
+    }
+    __syncthreads();
+    for (int o = 1; o < kBuckets; o <<= 1) {  // inclusive scan of the bucket totals, heaviest first
+        const uint32_t add = (q == 0 && k >= o) ? total[0][k - o] : 0u;
+        __syncthreads();
+        if (q == 0) total[0][k] += add;
+        __syncthreads();
+    }
+    if (q == 0) cur[k] = (k ? total[0][k - 1] : 0u) + before[0][k];
+    __syncthreads();
+    const long long r0 = (long long)c * chunk;
     const long long r1 = r0 + chunk < B ? r0 + chunk : B;
-    for (long long b = r0 + t; b < r1; b += kSchedThreads) perm[atomicAdd(&cur[key[b]], 1u)] = (int32_t)b;
+    for (long long b = r0 + t; b < r1; b += kScatThreads) perm[atomicAdd(&cur[key[b]], 1u)] = (int32_t)b;
 }
 
 // rows per chunk: at least kMinChunk, enough that there are at most kMaxChunks chunks
@@ -207,8 +199,8 @@ int launch_schedule(const uint8_t* sX, const uint8_t* sZ, long long B, int mX, i
     *perm_out = perm;
     hipLaunchKernelGGL(schedule_hist_kernel, dim3(nch), dim3(kHistThreads), 0, st, sX, sZ, B, mX, mZ, chunk, key,
                        counts, zero_flags);
-    hipLaunchKernelGGL(schedule_offsets_kernel, dim3(1), dim3(kOffThreads), 0, st, counts, nch);
-    hipLaunchKernelGGL(schedule_scatter_kernel, dim3(nch), dim3(kSchedThreads), 0, st, key, B, chunk, counts, perm);
+    hipLaunchKernelGGL(schedule_scatter_kernel, dim3(nch), dim3(kScatThreads), 0, st, key, B, chunk, nch, counts,
+                       perm);
     const hipError_t err = hipGetLastError();
     if (err != hipSuccess) return fail(QEC_ERR_HIP, std::string("schedule launch: ") + hipGetErrorString(err));
     return QEC_OK;

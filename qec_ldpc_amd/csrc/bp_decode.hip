@@ -95,6 +95,15 @@ namespace qec {
 #ifndef QEC_TRACK_FROM
 #define QEC_TRACK_FROM 2
 #endif
+//   QEC_LONG_PRIO    n > 0: a sector still running at iteration n (almost every sector has jumped
+//                    to its end by iteration 7) raises its wave's issue priority, so the few
+//                    never-hardening waves, which set the launch's tail, lose less time to the
+//                    waves sharing their SIMD (0: off; no effect beyond noise at n = 5..20:
+//                    profiles/r01/session7/cmp_s7d_*.txt -- those waves are latency-bound, not
+//                    starved of issue slots)
+#ifndef QEC_LONG_PRIO
+#define QEC_LONG_PRIO 0
+#endif
 #define QEC_PICK(macro, dflt) ((macro) >= 0 ? (macro) != 0 : (dflt))
 
 // Per-variant tuning: minimum waves per SIMD for the register allocator, and the options above.
@@ -816,6 +825,9 @@ __device__ __forceinline__ void decode_sector(const BpArgs& a, Lane& ln, long lo
     // iterations n .. N-2 (DecoderCPU.h:280-291); the last one is peeled below
     for (; n < N - 1; ++n) {
         if (!__any(active)) break;  // DecoderCPU.h:282 (fixed: only after a cycle jump)
+        if constexpr (QEC_LONG_PRIO > 0) {
+            if (n == QEC_LONG_PRIO) __builtin_amdgcn_s_setprio(3);
+        }
         if (active) {
             ++it;
             const bool was_hard = hard;

@@ -104,6 +104,16 @@ namespace qec {
 #ifndef QEC_LONG_PRIO
 #define QEC_LONG_PRIO 0
 #endif
+//   QEC_ROW_HARD     a soft sector's check pass takes the XOR form row by row: row r of the
+//                    var pass's outputs is tested for hardness on its own (one ballot per output
+//                    into a per-row SGPR mask instead of one OR into a lane register), and a row
+//                    whose every message is +0 or 1.0 is updated by check_pass_hard's rule.
+//                    Bit-identical but slower (P61 0.819 / 0.750 ms for modes 1 / 2 vs 0.706 ms:
+//                    profiles/r01/session7/cmp_s7e_*.txt, cmp_s7f_*.txt): rows rarely harden
+//                    before their whole sector does.  Off.
+#ifndef QEC_ROW_HARD
+#define QEC_ROW_HARD 0
+#endif
 #define QEC_PICK(macro, dflt) ((macro) >= 0 ? (macro) != 0 : (dflt))
 
 // Per-variant tuning: minimum waves per SIMD for the register allocator, and the options above.
@@ -361,10 +371,18 @@ __device__ __forceinline__ bool div_short_ok(float n, float d)
 // ---- one sector (X: R = J, Z: R = K) ------------------------------------
 // EqNodeUpdate (DecoderCPU.h:150-186) for checks (r, i), r = 0..R-1: lane-local.
 template <int R, int L>
-__device__ __forceinline__ void check_pass(float (&msg)[R][L], uint32_t sbits)
+__device__ __forceinline__ void check_pass(float (&msg)[R][L], uint32_t sbits, uint32_t hrows = 0)
 {
 #pragma unroll
     for (int r = 0; r < R; ++r) {
+        if (QEC_ROW_HARD && ((hrows >> r) & 1u)) {  // every message of row r is +0 or 1.0: see check_pass_hard
+            uint32_t x = ((sbits >> r) & 1u) ? 0x3F800000u : 0u;
+#pragma unroll
+            for (int l = 0; l < L; ++l) x ^= __float_as_uint(msg[r][l]);
+#pragma unroll
+            for (int l = 0; l < L; ++l) msg[r][l] = __uint_as_float(x ^ __float_as_uint(msg[r][l]));
+            continue;
+        }
         const float h = ((sbits >> r) & 1u) ? 0.5f : -0.5f;
         float av[L];
 #pragma unroll
@@ -420,11 +438,18 @@ __device__ __forceinline__ void check_pass_hard(float (&msg)[R][L], uint32_t sbi
 // equal (on every live lane), i.e. the new state passes var_pass_agree's test as it stands.
 template <int R, int L, int SEC, bool LAST, bool HD, class SH, class TU>
 __device__ __forceinline__ uint32_t var_pass(const BpArgs& a, float (&msg)[R][L], const Lane& ln, float pp,
-                                             float one_minus_pp, bool& hard, bool& vagree, bool track = true)
+                                             float one_minus_pp, bool& hard, bool& vagree, uint32_t& hrows,
+                                             bool track = true)
 {
     const bool hard_in = hard;
     bool vsame = true;  // this lane's variables: all R outputs equal (float compare: NaN is unequal)
     uint32_t soft_bits = 0;  // OR of bits(q - q*q) over outputs not known to be hard: 0 iff all are 0 or 1
+    // QEC_ROW_HARD 1: live lanes with a soft output in row r (wave masks, a ballot per output);
+    //              2: OR of bits(q - q*q) over row r's outputs (a lane register per row, R ballots)
+    unsigned long long rsoft[R];
+    uint32_t rbits[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) { rsoft[r] = 0ull; rbits[r] = 0u; }
     // the short division's guard assumes every message is a probability in [0, 1], which
     // holds by induction when p' is (DecoderCPU.h:135-229); other p' always take the full path
     const bool pp_ok = pp >= 0.0f && pp <= 1.0f;
@@ -550,7 +575,15 @@ __device__ __forceinline__ uint32_t var_pass(const BpArgs& a, float (&msg)[R][L]
         if constexpr (TU::kSaturate) {
             if (!zero && track) {
 #pragma unroll
-                for (int j = 0; j < ND; ++j) soft_bits |= __float_as_uint(__builtin_fmaf(-qd[j], qd[j], qd[j]));
+                for (int j = 0; j < ND; ++j) {
+                    const uint32_t sb = __float_as_uint(__builtin_fmaf(-qd[j], qd[j], qd[j]));
+                    if constexpr (QEC_ROW_HARD == 1 && !LAST)
+                        rsoft[j] |= __ballot(ln.live && sb != 0u);
+                    else if constexpr (QEC_ROW_HARD == 2 && !LAST)
+                        rbits[j] |= sb;
+                    else
+                        soft_bits |= sb;
+                }
 #pragma unroll
                 for (int j = 1; j < ND; ++j) vsame &= qd[j] == qd[0];
             }
@@ -571,7 +604,25 @@ __device__ __forceinline__ uint32_t var_pass(const BpArgs& a, float (&msg)[R][L]
         }
     }
     if constexpr (TU::kSaturate) {
-        hard = track && (a.hardPaths & QEC_HP_FORMS) && hard_ok(pp) && all_live(soft_bits == 0u, ln.live);
+        const bool forms = track && (a.hardPaths & QEC_HP_FORMS) && hard_ok(pp);
+        if constexpr (QEC_ROW_HARD == 2 && !LAST) {
+#pragma unroll
+            for (int r = 0; r < R; ++r) rsoft[r] = __ballot(ln.live && rbits[r] != 0u);
+        }
+        if constexpr (QEC_ROW_HARD && !LAST) {
+            unsigned long long any = 0ull;
+            uint32_t hr = 0;
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                any |= rsoft[r];
+                hr |= (uint32_t)(rsoft[r] == 0ull) << r;
+            }
+            hard = forms && any == 0ull;
+            hrows = forms ? hr : 0u;
+        } else {
+            hard = forms && all_live(soft_bits == 0u, ln.live);
+            hrows = 0u;
+        }
         vagree = hard && all_live(vsame, ln.live);
     }
     return hdmask;
@@ -643,7 +694,8 @@ __device__ __forceinline__ bool lane_syndrome_ok(const BpArgs& a, uint32_t hdmas
 // path, where the new state passed that test; tracked by var_pass otherwise).
 template <int R, int L, int SEC, int STOP, bool LAST, class SH, class TU>
 __device__ __forceinline__ bool iteration(const BpArgs& a, float (&msg)[R][L], uint32_t sbits, int n, Lane& ln,
-                                          float pp, float one_minus_pp, bool& hard, bool& agreed, bool& vagree)
+                                          float pp, float one_minus_pp, bool& hard, bool& agreed, bool& vagree,
+                                          uint32_t& hrows)
 {
     const int P = SH::P(a);
     // launder the permute bases so their per-rotation selects are recomputed inside the
@@ -659,12 +711,12 @@ __device__ __forceinline__ bool iteration(const BpArgs& a, float (&msg)[R][L], u
         if (agreed)
             vagree = true;
         else
-            hdmask = var_pass<R, L, SEC, LAST, HD, SH, TU>(a, msg, ln, pp, one_minus_pp, hard, vagree);
+            hdmask = var_pass<R, L, SEC, LAST, HD, SH, TU>(a, msg, ln, pp, one_minus_pp, hard, vagree, hrows);
     } else {
-        check_pass<R, L>(msg, sbits);
+        check_pass<R, L>(msg, sbits, hrows);
         // the hard-state test is skipped in the first QEC_TRACK_FROM iterations (they essentially
         // never end hard; skipping only delays the exact hard forms, never changes a bit)
-        hdmask = var_pass<R, L, SEC, LAST, HD, SH, TU>(a, msg, ln, pp, one_minus_pp, hard, vagree,
+        hdmask = var_pass<R, L, SEC, LAST, HD, SH, TU>(a, msg, ln, pp, one_minus_pp, hard, vagree, hrows,
                                                        LAST || n >= QEC_TRACK_FROM);
     }
     if constexpr (STOP == QEC_STOP_REF) {
@@ -815,6 +867,7 @@ __device__ __forceinline__ void decode_sector(const BpArgs& a, Lane& ln, long lo
     // can read it lane-locally
     bool in_agree = false, st_agreed = false;
     bool agreed = false, vagree = false;
+    uint32_t hrows = 0;  // QEC_ROW_HARD: rows of the current state whose every message is +0 or 1.0
     int ph_soft = 0, ph_hard = 0, ph_agree = 0, ph_jump = 0;  // QEC_PHASE_STATS
     if (QEC_TABLE0 && N >= 2 && active) {  // iteration 0 by table (see iteration0)
         ++it;
@@ -832,7 +885,7 @@ __device__ __forceinline__ void decode_sector(const BpArgs& a, Lane& ln, long lo
             ++it;
             const bool was_hard = hard;
             if (iteration<R, L, SEC, STOP, false, SH, TU>(a, msg, sbits, n, ln, pp, one_minus_pp, hard, agreed,
-                                                          vagree))
+                                                          vagree, hrows))
                 active = false;
             if constexpr (QEC_PHASE_STATS) { ph_soft += !was_hard; ph_hard += was_hard && !agreed; ph_agree += agreed; }
             if constexpr (TU::kSaturate) {
@@ -854,7 +907,7 @@ __device__ __forceinline__ void decode_sector(const BpArgs& a, Lane& ln, long lo
     if (n == N - 1 && active) {
         ++it;
         const bool was_hard = hard;
-        iteration<R, L, SEC, STOP, true, SH, TU>(a, msg, sbits, n, ln, pp, one_minus_pp, hard, agreed, vagree);
+        iteration<R, L, SEC, STOP, true, SH, TU>(a, msg, sbits, n, ln, pp, one_minus_pp, hard, agreed, vagree, hrows);
         if constexpr (QEC_PHASE_STATS) { ph_soft += !was_hard; ph_hard += was_hard && !agreed; ph_agree += agreed; }
         st_agreed = vagree;
     }

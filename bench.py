@@ -223,7 +223,11 @@ def main():
         out["iteration_histogram"] = {str(k): int(v) for k, v in enumerate(hist) if v}
 
     if world > 1 and not args.no_gather:
-        out["gather"] = gather_step(dec, eX, eZ, fl, B, world, rank, dev, stream)
+        # measured after the timed steps; a failure here must not cost the bench line
+        try:
+            out["gather"] = gather_step(dec, eX, eZ, fl, B, world, rank, dev, stream)
+        except Exception as exc:  # noqa: BLE001
+            out["gather"] = {"error": "%s: %s" % (type(exc).__name__, exc)}
 
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(code, fname, sX.cpu().numpy(), sZ.cpu().numpy(), p, iters, args, eX, eZ, fl)

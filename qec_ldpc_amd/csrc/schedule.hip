@@ -35,9 +35,11 @@ namespace qec {
 
 constexpr int kBuckets = 256;    // bucket k = 255 - min(weight, 255): 0 = heaviest
 constexpr int kHistThreads = 1024;
-constexpr int kHistSplit = 4;    // threads per syndrome in the weight pass
+// threads per syndrome in the weight pass: 4 for long rows (P61: 549 bytes), 1 for short ones
+// (P7: 42 bytes), where four threads would only multiply the waves of a latency-bound launch
+constexpr int kHistSplitLong = 4;
+constexpr int kShortRows = 128;  // mX + mZ up to this many bytes: one thread per syndrome
 constexpr int kMaxChunks = 1024;
-constexpr int kMinChunk = 256;   // rows per chunk
 constexpr int kMaxChunk = 4096;
 
 // Weight (bit 0 of each byte) of bytes [g0, g1) of s, read by one thread with 16-byte loads at
@@ -69,9 +71,9 @@ __device__ __forceinline__ uint32_t range_weight(const uint8_t* s, long long lo,
     return sum;
 }
 
-// ctr[0, 256): bucket totals, ctr[256, 512): bucket cursors (zeroed by the launch)
-// kHistSplit adjacent lanes per syndrome, each summing a quarter of its sX row and of its sZ
-// row; the quarters are added with lane shuffles
+// SPLIT adjacent lanes per syndrome, each summing a 1/SPLIT share of its sX row and of its sZ
+// row; the shares are added with lane shuffles
+template <int SPLIT>
 __global__ __launch_bounds__(kHistThreads) void schedule_hist_kernel(const uint8_t* __restrict__ sX,
                                                                    const uint8_t* __restrict__ sZ, long long B,
                                                                    int mX, int mZ, int chunk,
@@ -81,20 +83,20 @@ __global__ __launch_bounds__(kHistThreads) void schedule_hist_kernel(const uint8
 {
     __shared__ uint32_t h[kBuckets];
     const int t = threadIdx.x;
-    const int q = t % kHistSplit;
+    const int q = t % SPLIT;
     const long long r0 = (long long)blockIdx.x * chunk;
     const long long r1 = r0 + chunk < B ? r0 + chunk : B;
     if (t < kBuckets) h[t] = 0;
     __syncthreads();
-    for (long long b = r0 + t / kHistSplit; b - (t / kHistSplit) < r1; b += kHistThreads / kHistSplit) {
+    for (long long b = r0 + t / SPLIT; b - (t / SPLIT) < r1; b += kHistThreads / SPLIT) {
         uint32_t w = 0;
         if (b < r1) {
-            const long long x0 = b * mX + (long long)(mX * q / kHistSplit), x1 = b * mX + (long long)(mX * (q + 1) / kHistSplit);
-            const long long z0 = b * mZ + (long long)(mZ * q / kHistSplit), z1 = b * mZ + (long long)(mZ * (q + 1) / kHistSplit);
+            const long long x0 = b * mX + (long long)(mX * q / SPLIT), x1 = b * mX + (long long)(mX * (q + 1) / SPLIT);
+            const long long z0 = b * mZ + (long long)(mZ * q / SPLIT), z1 = b * mZ + (long long)(mZ * (q + 1) / SPLIT);
             w = range_weight(sX, x0, x1) + range_weight(sZ, z0, z1);
         }
 #pragma unroll
-        for (int o = 1; o < kHistSplit; o <<= 1) w += __shfl_xor(w, o);
+        for (int o = 1; o < SPLIT; o <<= 1) w += __shfl_xor(w, o);
         if (q == 0 && b < r1) {
             const int bk = kBuckets - 1 - (int)(w < kBuckets - 1 ? w : kBuckets - 1);
             key[b] = (uint8_t)bk;
@@ -163,11 +165,12 @@ __global__ __launch_bounds__(kScatThreads) void schedule_scatter_kernel(const ui
     for (long long b = r0 + t; b < r1; b += kScatThreads) perm[atomicAdd(&cur[key[b]], 1u)] = (int32_t)b;
 }
 
-// rows per chunk: at least kMinChunk, enough that there are at most kMaxChunks chunks
-static int chunk_of(long long B, int* nchunks)
+// rows per chunk: at least min_chunk (one pass of the histogram workgroup), enough that there
+// are at most kMaxChunks chunks
+static int chunk_of(long long B, int min_chunk, int* nchunks)
 {
     long long chunk = (B + kMaxChunks - 1) / kMaxChunks;
-    if (chunk < kMinChunk) chunk = kMinChunk;
+    if (chunk < min_chunk) chunk = min_chunk;
     *nchunks = (int)((B + chunk - 1) / chunk);
     return (int)chunk;
 }
@@ -190,15 +193,20 @@ int launch_schedule(const uint8_t* sX, const uint8_t* sZ, long long B, int mX, i
                     uint8_t* zero_flags, int32_t** perm_out, hipStream_t st)
 {
     if (B > schedule_max_batch()) return fail(QEC_ERR_ARG, "schedule: batch too large to order");
+    const bool shortrows = mX + mZ <= kShortRows;
     int nch = 0;
-    const int chunk = chunk_of(B, &nch);
+    const int chunk = chunk_of(B, kHistThreads / (shortrows ? 1 : kHistSplitLong), &nch);
     uint8_t* p = static_cast<uint8_t*>(ws);
     int32_t* perm = reinterpret_cast<int32_t*>(p);
     uint32_t* counts = reinterpret_cast<uint32_t*>(p + perm_bytes(B));
     uint8_t* key = reinterpret_cast<uint8_t*>(counts + (size_t)kMaxChunks * kBuckets);
     *perm_out = perm;
-    hipLaunchKernelGGL(schedule_hist_kernel, dim3(nch), dim3(kHistThreads), 0, st, sX, sZ, B, mX, mZ, chunk, key,
-                       counts, zero_flags);
+    if (shortrows)
+        hipLaunchKernelGGL(schedule_hist_kernel<1>, dim3(nch), dim3(kHistThreads), 0, st, sX, sZ, B, mX, mZ, chunk, key,
+                           counts, zero_flags);
+    else
+        hipLaunchKernelGGL(schedule_hist_kernel<kHistSplitLong>, dim3(nch), dim3(kHistThreads), 0, st, sX, sZ, B, mX, mZ,
+                           chunk, key, counts, zero_flags);
     hipLaunchKernelGGL(schedule_scatter_kernel, dim3(nch), dim3(kScatThreads), 0, st, key, B, chunk, nch, counts,
                        perm);
     const hipError_t err = hipGetLastError();

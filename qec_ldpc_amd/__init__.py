@@ -80,6 +80,13 @@ def lib():
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             raise QecError("libqecldpc.so not built (%s); run `make` or __graft_entry__.build()" % LIB_PATH)
+        # One HIP runtime per process: torch ships its own libamdhip64 (soname .so.7, file name
+        # .so).  Loaded first, it also serves this library's libamdhip64.so.7; loaded after
+        # /opt/rocm's copy, it is a second runtime in the process and torch then sees no GPU.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = ctypes.CDLL(LIB_PATH)
         vp, i, f, sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_size_t
         sig = {

@@ -300,3 +300,39 @@ def test_schedule_workspace_across_calls(env):
                 assert np.array_equal(a, b), "B=%d" % B
     finally:
         dec.set_option("schedule", 1)
+
+
+@pytest.mark.parametrize("key,B", [("P7", 70001), ("P7", 1024 * 1024 + 3), ("P61", 70001), ("P61", 300001)])
+def test_schedule_covers_every_syndrome(env, key, B):
+    """The order pass (schedule.hip) is a permutation of the batch: with output buffers
+    that start as garbage, an ordered decode writes every syndrome's eX, eZ, flags and
+    iterations exactly as the batch-order decode does.  Sizes cover both histogram shapes
+    (short rows: one thread per syndrome, 1 024-syndrome chunks; long rows: four threads,
+    256-syndrome chunks), a ragged last chunk, and chunks longer than one histogram pass
+    (more than 1 024 chunks' worth of minimum-size chunks)."""
+    import torch
+    code, dec, _ = env[key]
+    dev = torch.device("cuda", 0)
+    x = torch.empty((B, code.n), dtype=torch.uint8, device=dev)
+    z = torch.empty((B, code.n), dtype=torch.uint8, device=dev)
+    sX = torch.empty((B, code.numEqsX), dtype=torch.uint8, device=dev)
+    sZ = torch.empty((B, code.numEqsZ), dtype=torch.uint8, device=dev)
+    dec.sample_depolarizing_dev(7 + B, 0, 0.03, x, z)
+    dec.syndrome_dev(x, z, sX, sZ)
+    del x, z
+    outs = []
+    for sched in (0, 2):
+        o = [torch.full((B, code.n), 0xA5, dtype=torch.uint8, device=dev),
+             torch.full((B, code.n), 0xA5, dtype=torch.uint8, device=dev),
+             torch.full((B,), 0xA5, dtype=torch.uint8, device=dev),
+             torch.full((B, 2), -7, dtype=torch.int32, device=dev)]
+        dec.set_option("schedule", sched)
+        try:
+            dec.decode_batch_dev(sX, sZ, 0.03, 12, "ref", *o)
+            torch.cuda.synchronize()
+        finally:
+            dec.set_option("schedule", 1)
+        outs.append(o)
+    assert int(outs[0][3].min()) >= 1  # batch order wrote every syndrome
+    for name, a, b in zip(("eX", "eZ", "flags", "iters"), outs[0], outs[1]):
+        assert torch.equal(a, b), "%s B=%d: %s differs between batch and dispatch order" % (key, B, name)

@@ -118,9 +118,11 @@ namespace qec {
 
 // Per-variant tuning: minimum waves per SIMD for the register allocator, and the options above.
 template <int MINW_, bool RELABEL_, bool ZEROSKIP_, bool FASTDIV_, bool SATURATE_ = false, bool SPLIT_ = false,
-          bool MASKSEL_ = false, int PIPE_ = 0>
+          bool MASKSEL_ = false, int PIPE_ = 0, int WPB_ = 4, int SYNW_ = 0>
 struct Tune {
     static constexpr int kMinWaves = MINW_;
+    static constexpr int kMinWavesSyn = SYNW_ > 0 ? SYNW_ : MINW_;  // the syndrome-stop kernels
+    static constexpr int kWavesPerBlock = WPB_;  // waves per workgroup (QEC_WAVES_PER_BLOCK overrides)
     static constexpr bool kMaskSelect = QEC_PICK(QEC_MASK_SELECT, MASKSEL_);
     static constexpr int kPipeline = QEC_PIPELINE >= 0 ? QEC_PIPELINE : PIPE_;
     static constexpr bool kSplit = SPLIT_;  // QEC_OPT_SECTOR_SPLIT = 1 (auto) splits sectors for this variant
@@ -974,7 +976,7 @@ __device__ __forceinline__ void decode_sector(const BpArgs& a, Lane& ln, long lo
 
 // Tuning knobs (compile-time; tools/kbench/ sweeps them).
 #ifndef QEC_WAVES_PER_BLOCK
-#define QEC_WAVES_PER_BLOCK 4
+#define QEC_WAVES_PER_BLOCK 0   // 0: per-variant (Tune<>::kWavesPerBlock)
 #endif
 #ifndef QEC_MIN_WAVES_PER_EU
 #define QEC_MIN_WAVES_PER_EU 0  // 0: per-variant defaults below
@@ -987,9 +989,13 @@ __device__ __forceinline__ void decode_sector(const BpArgs& a, Lane& ln, long lo
 // per variant with tools/kbench (P61: 5 waves beat 4 by 4 %; see profiles/).
 // SPLIT: waves 2k and 2k+1 decode sectors X and Z of group k (adjacent waves, one workgroup);
 // the launch zeroed flags[] and each sector ORs in its bits.  Otherwise one wave decodes both.
+template <class TU>
+constexpr int waves_per_block() { return QEC_WAVES_PER_BLOCK > 0 ? QEC_WAVES_PER_BLOCK : TU::kWavesPerBlock; }
+
 template <int RX, int RZ, int L, int STOP, class SH, class TU, bool SPLIT>
-__global__ __launch_bounds__(64 * QEC_WAVES_PER_BLOCK,
-                             (QEC_MIN_WAVES_PER_EU ? QEC_MIN_WAVES_PER_EU : TU::kMinWaves) +
+__global__ __launch_bounds__(64 * waves_per_block<TU>(),
+                             (QEC_MIN_WAVES_PER_EU ? QEC_MIN_WAVES_PER_EU
+                                                   : STOP == QEC_STOP_SYNDROME ? TU::kMinWavesSyn : TU::kMinWaves) +
                                  (STOP == QEC_STOP_SYNDROME ? QEC_SYN_MINW_DELTA : 0))
 void bp_decode_kernel(const BpArgs a)
 {
@@ -1054,6 +1060,7 @@ struct Variant {
     int P, sigma, tau;  // P > 0: specialised to the generator's tables for these parameters
     bool relabel;       // runtime-shift variants: relabel the lane tables at launch
     bool split_auto;    // QEC_OPT_SECTOR_SPLIT = 1 takes the split kernels
+    int waves_per_block;
     KernelFn fn[3];     // indexed by stop rule
     KernelFn split[3];  // the same with one wave per sector (nullptr: not instantiated)
     const char* name;
@@ -1062,7 +1069,7 @@ struct Variant {
 template <int J, int K, int L, class SH, class TU, bool WITH_SPLIT>
 static Variant make_variant(int P, int S, int T, const char* name)
 {
-    Variant v{J, K, L, P, S, T, TU::kRelabel, TU::kSplit && WITH_SPLIT,
+    Variant v{J, K, L, P, S, T, TU::kRelabel, TU::kSplit && WITH_SPLIT, waves_per_block<TU>(),
               {bp_decode_kernel<J, K, L, QEC_STOP_REF, SH, TU, false>,
                bp_decode_kernel<J, K, L, QEC_STOP_FIXED, SH, TU, false>,
                bp_decode_kernel<J, K, L, QEC_STOP_SYNDROME, SH, TU, false>},
@@ -1075,7 +1082,8 @@ static Variant make_variant(int P, int S, int T, const char* name)
     }
     return v;
 }
-// Tune<min waves per SIMD, relabel, zero-skip, short division, hard-message paths>
+// Tune<min waves per SIMD, relabel, zero-skip, short division, hard-message paths, sector split,
+//      mask-select rotation bases, gather pipelining depth, waves per workgroup, min waves (syndrome stop)>
 template <int J, int K, int L, class TU = Tune<1, false, true, true, true>>
 static Variant rt()
 {
@@ -1096,10 +1104,13 @@ static Variant gen()
 // @ p=0.01, 2.45 vs 2.81 ms @ p=0.05; session-5 kbench, profiles/r01/session5/cmp_s5m_*.txt),
 // and once the hoisted rotation bases spill, selecting them by lane mask wins (P61 0.855 vs
 // 0.963 ms, cmp_s5o/s5p).  With the 6-instruction short division and the min-reduced guard P7
-// takes the short division again (0.090 vs 0.092 ms, cmp_s6j).
+// takes the short division again (0.090 vs 0.092 ms, cmp_s6j).  P61 then moves to 5 waves per
+// SIMD (96 VGPRs, a few spills) and 2-wave workgroups: fixed stop 0.728 vs 0.751 ms at p = 0.01,
+// 1.75 vs 2.16 ms at p = 0.05; its syndrome-stop kernels spill badly at 5 waves (450 scratch
+// loads, 1.01 vs 0.50 ms) and keep 4 (profiles/r01/session7/cmp_s7l-n_*.txt).
 static const Variant kVariants[] = {
     // specialised: the two code files the reference ships
-    gen<4, 5, 10, 61, 9, 49, Tune<4, true, false, true, true, false, true, 1>>(),
+    gen<4, 5, 10, 61, 9, 49, Tune<5, true, false, true, true, false, true, 1, 2, 4>>(),
     gen<3, 3, 6, 7, 2, 3, Tune<8, false, false, true, true, true>>(),
 #ifndef QEC_KBENCH_MINIMAL  // experiment builds (tools/kbench) only compile the shipped-code kernels
     // runtime shifts, any P <= 64 with these block shapes
@@ -1169,7 +1180,7 @@ int launch_decode(const void* variant, const Code& c, const uint8_t* sX, const u
     a.hardPaths = hardPaths;
     relabel(c.EX.data(), c.J, c.L, c.P, v->relabel, a.SX, a.DX, a.CX);
     relabel(c.EZ.data(), c.K, c.L, c.P, v->relabel, a.SZ, a.DZ, a.CZ);
-    const int wavesPerBlock = QEC_WAVES_PER_BLOCK;
+    const int wavesPerBlock = v->waves_per_block;
     const long long waves = (B + a.G - 1) / a.G * (split ? 2 : 1);
     const long long blocks = (waves + wavesPerBlock - 1) / wavesPerBlock;
     if (blocks > 0x7fffffffLL) return fail(QEC_ERR_ARG, "batch too large for one launch");

@@ -7,7 +7,7 @@ HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -fno-f
 CSRC     := qec_ldpc_amd/csrc
 OBJ      := build/obj
 LIB      := qec_ldpc_amd/libqecldpc.so
-OBJS     := $(OBJ)/bp_decode.o $(OBJ)/bp_sparse.o $(OBJ)/schedule.o $(OBJ)/montecarlo.o $(OBJ)/code_model.o $(OBJ)/capi.o
+OBJS     := $(OBJ)/bp_decode.o $(OBJ)/bp_decode_p61.o $(OBJ)/bp_sparse.o $(OBJ)/schedule.o $(OBJ)/montecarlo.o $(OBJ)/code_model.o $(OBJ)/capi.o
 HDRS     := include/qec_ldpc.h include/HostDeviceArray.h $(CSRC)/qec_internal.h
 
 all: $(LIB) oracle tools/qec_ldpc
@@ -17,6 +17,10 @@ $(OBJ):
 
 $(OBJ)/bp_decode.o: $(CSRC)/bp_decode.hip $(HDRS) | $(OBJ)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+# the P61 reference/fixed-stop kernels under the iterative-minreg scheduler (bp_decode.hip, TuneP61)
+$(OBJ)/bp_decode_p61.o: $(CSRC)/bp_decode_p61.hip $(CSRC)/bp_decode.hip $(HDRS) | $(OBJ)
+	$(HIPCC) $(HIPFLAGS) -mllvm -amdgpu-sched-strategy=iterative-minreg -c $< -o $@
 
 $(OBJ)/bp_sparse.o: $(CSRC)/bp_sparse.hip $(HDRS) | $(OBJ)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@

@@ -1055,6 +1055,34 @@ void bp_decode_kernel(const BpArgs a)
 // ---- variant table ----------------------------------------------------------
 using KernelFn = void (*)(const BpArgs);
 
+// The P61 tuning.  Its reference- and fixed-stop kernels are also compiled in a second
+// translation unit, bp_decode_p61.hip, under LLVM's iterative-minreg scheduler (the flag is
+// per file): 15 instead of 42 spill reloads at 96 VGPRs, fixed stop 0.656 vs 0.700 ms, reference
+// stop 0.567 vs 0.613 ms; its syndrome-stop kernel spills more that way (0.517 vs 0.476 ms)
+// and P7 gains nothing, so only those two kernels come from there
+// (profiles/r01/session7/cmp_s7u_*.txt, cmp_s7v_*.txt).  A distinct Tune type keeps the two
+// units' kernels apart (same code, different symbols).
+using TuneP61 = Tune<5, true, false, true, true, false, true, 1, 2, 4>;
+struct TuneP61MinReg : TuneP61 {};
+using ShiftsP61 = GeneratedShifts<4, 5, 10, 61, 9, 49, TuneP61::kRelabel, TuneP61::kMaskSelect>;
+#ifndef QEC_P61_MINREG
+#define QEC_P61_MINREG 1
+#endif
+KernelFn p61_minreg_kernel(int stop, bool split);  // bp_decode_p61.hip
+
+#ifdef QEC_P61_MINREG_TU
+KernelFn p61_minreg_kernel(int stop, bool split)
+{
+    if (stop == QEC_STOP_REF)
+        return split ? bp_decode_kernel<4, 5, 10, QEC_STOP_REF, ShiftsP61, TuneP61MinReg, true>
+                     : bp_decode_kernel<4, 5, 10, QEC_STOP_REF, ShiftsP61, TuneP61MinReg, false>;
+    if (stop == QEC_STOP_FIXED)
+        return split ? bp_decode_kernel<4, 5, 10, QEC_STOP_FIXED, ShiftsP61, TuneP61MinReg, true>
+                     : bp_decode_kernel<4, 5, 10, QEC_STOP_FIXED, ShiftsP61, TuneP61MinReg, false>;
+    return nullptr;
+}
+#else
+
 struct Variant {
     int J, K, L;
     int P, sigma, tau;  // P > 0: specialised to the generator's tables for these parameters
@@ -1108,9 +1136,21 @@ static Variant gen()
 // SIMD (96 VGPRs, a few spills) and 2-wave workgroups: fixed stop 0.728 vs 0.751 ms at p = 0.01,
 // 1.75 vs 2.16 ms at p = 0.05; its syndrome-stop kernels spill badly at 5 waves (450 scratch
 // loads, 1.01 vs 0.50 ms) and keep 4 (profiles/r01/session7/cmp_s7l-n_*.txt).
+static Variant gen_p61()
+{
+    Variant v = gen<4, 5, 10, 61, 9, 49, TuneP61>();
+    if (QEC_P61_MINREG) {
+        for (int stop : {QEC_STOP_REF, QEC_STOP_FIXED}) {
+            v.fn[stop] = p61_minreg_kernel(stop, false);
+            v.split[stop] = p61_minreg_kernel(stop, true);
+        }
+    }
+    return v;
+}
+
 static const Variant kVariants[] = {
     // specialised: the two code files the reference ships
-    gen<4, 5, 10, 61, 9, 49, Tune<5, true, false, true, true, false, true, 1, 2, 4>>(),
+    gen_p61(),
     gen<3, 3, 6, 7, 2, 3, Tune<8, false, false, true, true, true>>(),
 #ifndef QEC_KBENCH_MINIMAL  // experiment builds (tools/kbench) only compile the shipped-code kernels
     // runtime shifts, any P <= 64 with these block shapes
@@ -1189,5 +1229,7 @@ int launch_decode(const void* variant, const Code& c, const uint8_t* sX, const u
     if (err != hipSuccess) return fail(QEC_ERR_HIP, std::string("bp_decode launch: ") + hipGetErrorString(err));
     return QEC_OK;
 }
+
+#endif  // QEC_P61_MINREG_TU
 
 }  // namespace qec

@@ -24,7 +24,9 @@ build() {
   out=build/variants/$name
   mkdir -p $out
   $HIPCC $BASE -DQEC_KBENCH_MINIMAL "$@" -c qec_ldpc_amd/csrc/bp_decode.hip -o $out/bp_decode.o
-  $HIPCC --offload-arch=gfx950 -shared -fPIC -o $out/libqecldpc.so $out/bp_decode.o $COMMON/*.o
+  $HIPCC $BASE -DQEC_KBENCH_MINIMAL -mllvm -amdgpu-sched-strategy=iterative-minreg "$@" \
+      -c qec_ldpc_amd/csrc/bp_decode_p61.hip -o $out/bp_decode_p61.o
+  $HIPCC --offload-arch=gfx950 -shared -fPIC -o $out/libqecldpc.so $out/bp_decode.o $out/bp_decode_p61.o $COMMON/*.o
   echo "built $name"
 }
 pids=()

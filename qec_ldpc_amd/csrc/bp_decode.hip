@@ -1058,17 +1058,21 @@ using KernelFn = void (*)(const BpArgs);
 // The P61 tuning.  Its reference- and fixed-stop kernels are also compiled in a second
 // translation unit, bp_decode_p61.hip, under LLVM's iterative-minreg scheduler (the flag is
 // per file): 15 instead of 42 spill reloads at 96 VGPRs, fixed stop 0.656 vs 0.700 ms, reference
-// stop 0.567 vs 0.613 ms; its syndrome-stop kernel spills more that way (0.517 vs 0.476 ms)
-// and P7 gains nothing, so only those two kernels come from there
-// (profiles/r01/session7/cmp_s7u_*.txt, cmp_s7v_*.txt).  A distinct Tune type keeps the two
-// units' kernels apart (same code, different symbols).
+// stop 0.567 vs 0.613 ms; its syndrome-stop kernel spills more that way (0.517 vs 0.476 ms).
+// P7's fixed and reference stops gain nothing, but its syndrome stop does (0.087 vs 0.100 ms)
+// (profiles/r01/session7/cmp_s7u_*.txt, cmp_s7v_*.txt).  So those kernels come from there.
+// A distinct Tune type keeps the two units' kernels apart (same code, different symbols).
 using TuneP61 = Tune<5, true, false, true, true, false, true, 1, 2, 4>;
 struct TuneP61MinReg : TuneP61 {};
 using ShiftsP61 = GeneratedShifts<4, 5, 10, 61, 9, 49, TuneP61::kRelabel, TuneP61::kMaskSelect>;
+using TuneP7 = Tune<8, false, false, true, true, true>;
+struct TuneP7MinReg : TuneP7 {};
+using ShiftsP7 = GeneratedShifts<3, 3, 6, 7, 2, 3, TuneP7::kRelabel, TuneP7::kMaskSelect>;
 #ifndef QEC_P61_MINREG
 #define QEC_P61_MINREG 1
 #endif
 KernelFn p61_minreg_kernel(int stop, bool split);  // bp_decode_p61.hip
+KernelFn p7_minreg_kernel(int stop, bool split);   // bp_decode_p61.hip
 
 #ifdef QEC_P61_MINREG_TU
 KernelFn p61_minreg_kernel(int stop, bool split)
@@ -1079,6 +1083,13 @@ KernelFn p61_minreg_kernel(int stop, bool split)
     if (stop == QEC_STOP_FIXED)
         return split ? bp_decode_kernel<4, 5, 10, QEC_STOP_FIXED, ShiftsP61, TuneP61MinReg, true>
                      : bp_decode_kernel<4, 5, 10, QEC_STOP_FIXED, ShiftsP61, TuneP61MinReg, false>;
+    return nullptr;
+}
+KernelFn p7_minreg_kernel(int stop, bool split)
+{
+    if (stop == QEC_STOP_SYNDROME)
+        return split ? bp_decode_kernel<3, 3, 6, QEC_STOP_SYNDROME, ShiftsP7, TuneP7MinReg, true>
+                     : bp_decode_kernel<3, 3, 6, QEC_STOP_SYNDROME, ShiftsP7, TuneP7MinReg, false>;
     return nullptr;
 }
 #else
@@ -1148,10 +1159,20 @@ static Variant gen_p61()
     return v;
 }
 
+static Variant gen_p7()
+{
+    Variant v = gen<3, 3, 6, 7, 2, 3, TuneP7>();
+    if (QEC_P61_MINREG) {
+        v.fn[QEC_STOP_SYNDROME] = p7_minreg_kernel(QEC_STOP_SYNDROME, false);
+        v.split[QEC_STOP_SYNDROME] = p7_minreg_kernel(QEC_STOP_SYNDROME, true);
+    }
+    return v;
+}
+
 static const Variant kVariants[] = {
     // specialised: the two code files the reference ships
     gen_p61(),
-    gen<3, 3, 6, 7, 2, 3, Tune<8, false, false, true, true, true>>(),
+    gen_p7(),
 #ifndef QEC_KBENCH_MINIMAL  // experiment builds (tools/kbench) only compile the shipped-code kernels
     // runtime shifts, any P <= 64 with these block shapes
     rt<4, 5, 10>(),

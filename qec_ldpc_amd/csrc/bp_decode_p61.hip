@@ -1,4 +1,4 @@
-// The P61 reference- and fixed-stop decode kernels, compiled with LLVM's iterative-minreg
+// The P61 reference- and fixed-stop and the P7 syndrome-stop decode kernels, compiled with LLVM's iterative-minreg
 // machine scheduler (Makefile: -mllvm -amdgpu-sched-strategy=iterative-minreg, a per-file
 // option).  Same source as bp_decode.hip; see the TuneP61 comment there for why and the
 // measurements.

@@ -37,7 +37,12 @@ constexpr int kBuckets = 256;    // bucket k = 255 - min(weight, 255): 0 = heavi
 constexpr int kHistThreads = 1024;
 // threads per syndrome in the weight pass: 4 for long rows (P61: 549 bytes), 1 for short ones
 // (P7: 42 bytes), where four threads would only multiply the waves of a latency-bound launch
-constexpr int kHistSplitLong = 4;
+// (QEC_HIST_SPLIT = 8, one round of loads per thread for P61, is slower: 23.8 vs 17.1 us,
+// profiles/r01/session7/rocprof_hist_split_s7bb.csv)
+#ifndef QEC_HIST_SPLIT
+#define QEC_HIST_SPLIT 4
+#endif
+constexpr int kHistSplitLong = QEC_HIST_SPLIT;
 constexpr int kShortRows = 128;  // mX + mZ up to this many bytes: one thread per syndrome
 constexpr int kMaxChunks = 1024;
 constexpr int kMaxChunk = 4096;
@@ -195,7 +200,7 @@ int launch_schedule(const uint8_t* sX, const uint8_t* sZ, long long B, int mX, i
     if (B > schedule_max_batch()) return fail(QEC_ERR_ARG, "schedule: batch too large to order");
     const bool shortrows = mX + mZ <= kShortRows;
     int nch = 0;
-    const int chunk = chunk_of(B, kHistThreads / (shortrows ? 1 : kHistSplitLong), &nch);
+    const int chunk = chunk_of(B, shortrows ? kHistThreads : 256, &nch);
     uint8_t* p = static_cast<uint8_t*>(ws);
     int32_t* perm = reinterpret_cast<int32_t*>(p);
     uint32_t* counts = reinterpret_cast<uint32_t*>(p + perm_bytes(B));

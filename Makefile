@@ -7,10 +7,10 @@ HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -fno-f
 CSRC     := qec_ldpc_amd/csrc
 OBJ      := build/obj
 LIB      := qec_ldpc_amd/libqecldpc.so
-OBJS     := $(OBJ)/bp_decode.o $(OBJ)/bp_decode_p61.o $(OBJ)/bp_sparse.o $(OBJ)/schedule.o $(OBJ)/montecarlo.o $(OBJ)/code_model.o $(OBJ)/capi.o
-HDRS     := include/qec_ldpc.h include/HostDeviceArray.h $(CSRC)/qec_internal.h
+OBJS     := $(OBJ)/bp_decode.o $(OBJ)/bp_decode_p61.o $(OBJ)/bp_decode_phase.o $(OBJ)/bp_sparse.o $(OBJ)/schedule.o $(OBJ)/montecarlo.o $(OBJ)/code_model.o $(OBJ)/capi.o
+HDRS     := include/qec_ldpc.h include/HostDeviceArray.h $(CSRC)/qec_internal.h $(CSRC)/qec_device.h
 
-all: $(LIB) oracle tools/qec_ldpc
+all: $(LIB) oracle tools/qec_ldpc tools/getstats_check
 
 $(OBJ):
 	mkdir -p $(OBJ)
@@ -21,6 +21,10 @@ $(OBJ)/bp_decode.o: $(CSRC)/bp_decode.hip $(HDRS) | $(OBJ)
 # the P61 reference/fixed-stop kernels under the iterative-minreg scheduler (bp_decode.hip, TuneP61)
 $(OBJ)/bp_decode_p61.o: $(CSRC)/bp_decode_p61.hip $(CSRC)/bp_decode.hip $(HDRS) | $(OBJ)
 	$(HIPCC) $(HIPFLAGS) -mllvm -amdgpu-sched-strategy=iterative-minreg -c $< -o $@
+
+# the instrumented kernels of QEC_OPT_PHASE_STATS (bp_decode.hip, QEC_PHASE_STATS)
+$(OBJ)/bp_decode_phase.o: $(CSRC)/bp_decode_phase.hip $(CSRC)/bp_decode.hip $(HDRS) | $(OBJ)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(OBJ)/bp_sparse.o: $(CSRC)/bp_sparse.hip $(HDRS) | $(OBJ)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
@@ -44,11 +48,15 @@ $(LIB): $(OBJS)
 tools/qec_ldpc: tools/qec_ldpc_main.cpp include/*.h $(LIB)
 	$(HIPCC) -O2 -std=c++17 -Iinclude -o $@ $< -Lqec_ldpc_amd -lqecldpc -Wl,-rpath,'$$ORIGIN/../qec_ldpc_amd'
 
+# DecoderGPU::GetStats vs GetStatistics through the C++ interface (tests/test_gpu_kat.py)
+tools/getstats_check: tools/getstats_check.cpp include/*.h $(LIB)
+	$(HIPCC) -O2 -std=c++17 -Iinclude -o $@ $< -Lqec_ldpc_amd -lqecldpc -Wl,-rpath,'$$ORIGIN/../qec_ldpc_amd'
+
 oracle:
 	$(MAKE) -s -C oracle
 
 clean:
-	rm -rf build $(LIB) tools/qec_ldpc
+	rm -rf build $(LIB) tools/qec_ldpc tools/getstats_check
 	$(MAKE) -s -C oracle clean
 
 .PHONY: all oracle clean

@@ -1,31 +1,39 @@
-"""Headline benchmark: syndromes decoded per second at a fixed number of BP
-iterations (BASELINE.json "metric"), on N MI355X with one process per GPU.
+"""Headline benchmark: syndromes decoded per second at a fixed number of BP iterations
+(BASELINE.json "metric"), on N MI355X with one process per GPU.
 
-One step = one batched decode (both sectors, `--iters` fixed iterations, reference
-update rules) of the rank's resident batch of synthetic depolarising syndromes.
-Inputs are generated and copied to HBM before the timed region.  Ranks decode
-disjoint shards of the sample index space; there is no collective in the data
-path (syndromes are independent), only the timing barrier and a MAX reduction.
+Workload (BASELINE.json configs[3]): the J=4,K=5,L=10,P=61 code, a global batch of 2^20
+depolarising syndromes (p = 0.01), 50 fixed BP iterations, sharded contiguously over the N
+GPUs: rank g decodes samples [g B / N, (g + 1) B / N) (strong scaling: the same 2^20 syndromes
+at every N).  `--batch` instead fixes the per-GPU batch (weak scaling), labelled as such.
+
+One step = one batched decode of the rank's resident shard (both sectors, reference update
+rules, exactly `--iters` iterations) writing bit-packed decision records (eX bits, eZ bits,
+flags byte: SURVEY.md 8(d)'s I/O model).  Syndromes are generated on the device (fused
+Philox sampler + syndrome kernel) before the timed region.  There is no collective in the
+decode step (syndromes are independent); at N > 1 the RCCL gather of every rank's records to
+rank 0 is timed separately, as its own component and end to end (decode + gather per step).
 
 Prints one JSON line (rank 0).  Extra objects:
-  roofline      -- the decode kernel's algorithmic bytes (16 B per
-                   edge-iteration + bit-packed I/O, i.e. an HBM-resident flooding
-                   schedule) over its HIP-event-timed launch duration, vs 8 TB/s;
-                   the engine keeps messages in VGPRs, so frac > 1 means it moves
-                   less than that schedule's bytes.
-  full_arithmetic -- the same batch re-timed with QEC_OPT_HARD_PATHS off (every
-                   iteration in full fp32 arithmetic, no hard-message forms), with a
-                   bit-identity check against the timed run's outputs.
-  no_cycle_jump -- the same with only QEC_OPT_CYCLE_JUMP off (hard-message forms, but
-                   every iteration executed one by one), also bit-identity checked.
-  valu          -- analytical full-arithmetic VALU lane-ops per launch over the
-                   full_arithmetic launch time, vs the fp32 VALU issue ceiling (on the
-                   hard-path launch the analytical count would over-count the work).
-  cpu_baseline  -- oracle (CPU restatement of DecoderCPU, OpenMP) on host cores,
-                   rank 0 at N = 1 only, bounded sample of the same workload.
+  roofline        the dominant kernel (the decode) against its real bound, VALU issue:
+                  SQ_INSTS_VALU per launch (rocprofv3 PMC, profiles/pmc_<code>.json, per syndrome
+                  x the batch) x 2 cycles / (1024 SIMDs x 2.4 GHz x launch time), launch time
+                  from HIP events on the launch stream in this run; traffic = PMC HBM bytes.
+  roofline_hbm_alg  SURVEY.md 8(d)'s HBM-resident flooding-schedule bytes over the launch time:
+                  valid only if frac <= 1 (the engine keeps messages in VGPRs and takes exact
+                  shortcuts, so it does far less than that schedule's traffic).
+  value_full_arithmetic / full_arithmetic  the same batch re-timed with every iteration in full
+                  fp32 arithmetic (QEC_OPT_HARD_PATHS = 0), bit-identity checked: the "50 BP
+                  iterations executed" rate.
+  sector_iterations  executed sector-iterations of one launch by phase (soft / hard / agreed /
+                  jumped), from the instrumented kernel (QEC_OPT_PHASE_STATS).
+  sustained       a >= 1 s window of the same step (clock-settled rate).
+  cpu_baseline    the oracle (CPU restatement of DecoderCPU, OpenMP) on host cores, rank 0 at
+                  N = 1 only, bounded sample of the same workload; also 1 thread and
+                  BASELINE configs[0] (P7, 1k syndromes, 20 iterations).
 """
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -36,23 +44,25 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 CODES = {
-    # name: (code file, default p, default iters, config label)
-    "p61": ("J_4_K_5_L_10_P_61_s_9_t_49", 0.01, 50,
-            "BASELINE configs[2]: J=4,K=5,L=10,P=61 code, batch 65536 per GPU, 50 fixed BP iters"),
-    "p7": ("J_3_K_3_L_6_P_7_s_2_t_3", 0.02, 20,
-           "BASELINE configs[1]: J=3,K=3,L=6,P=7 code, batch 65536 per GPU, 20 fixed BP iters"),
+    # name: (code file, default p, default iters)
+    "p61": ("J_4_K_5_L_10_P_61_s_9_t_49", 0.01, 50),
+    "p7": ("J_3_K_3_L_6_P_7_s_2_t_3", 0.02, 20),
 }
 SEED = 0x51EC0DE
+GLOBAL_BATCH = 1 << 20          # BASELINE configs[3]
 HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md, chip-level parameters
 VALU_PEAK_TOPS = 78.64          # 256 CU x 4 SIMD x 32 lanes x 2.4 GHz lane-ops/s (fp32 non-FMA issue ceiling)
+SIMDS = 1024                    # 256 CU x 4 SIMD
+CLOCK_GHZ = 2.4                 # peak engine clock
+VALU_ISSUE_CYCLES = 2           # one wave64 VALU instruction per 2 cycles on a SIMD-32 (MI355X_MICROARCH.md)
 
 
-def algorithmic_bytes_per_syndrome(code, iters):
+def algorithmic_bytes_per_syndrome(code, it_x, it_z):
     """16 B per edge-iteration (q read + r write, r read + q write)
     plus bit-packed I/O (syndrome bits in, correction bits out, one flag byte)."""
     EX, EZ = code.numEqsX * code.L, code.numEqsZ * code.L
     io = -(-(code.numEqsX + code.numEqsZ) // 8) + -(-(2 * code.n) // 8) + 1
-    return 16 * (EX + EZ) * iters + io
+    return 16 * (EX * it_x + EZ * it_z) + io
 
 
 def lane_ops_per_syndrome(code, iters):
@@ -71,23 +81,44 @@ def lane_ops_per_syndrome(code, iters):
     return per_iter * iters
 
 
+def shard(total, rank, world):
+    return total * rank // world, total * (rank + 1) // world
+
+
+def load_pmc(code_name, iters, stop, p):
+    """profiles/pmc_<code>.json if it was collected on this workload (code, iters, stop, p)."""
+    path = os.path.join(ROOT, "profiles", "pmc_%s.json" % code_name)
+    try:
+        with open(path) as f:
+            pm = json.load(f)
+    except (OSError, ValueError):
+        return None, path
+    if pm.get("iters") != iters or pm.get("stop") != stop or abs(float(pm.get("p", -1)) - p) > 1e-12:
+        return None, path
+    return pm, path
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=None, help="timed steps (default: enough for a >= 1 s window)")
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--code", choices=sorted(CODES), default="p61")
-    ap.add_argument("--batch", type=int, default=65536, help="syndromes per GPU per step")
+    ap.add_argument("--global-batch", type=int, default=GLOBAL_BATCH,
+                    help="syndromes per step over all GPUs (strong scaling)")
+    ap.add_argument("--batch", type=int, default=None, help="syndromes per GPU per step (weak scaling instead)")
     ap.add_argument("--iters", type=int, default=None)
     ap.add_argument("--p", type=float, default=None)
     ap.add_argument("--stop", choices=["fixed", "ref", "syndrome"], default="fixed")
+    ap.add_argument("--output", choices=["packed", "bytes"], default="packed",
+                    help="decision records (default) or eX/eZ/flags byte arrays")
+    ap.add_argument("--min-seconds", type=float, default=1.0, help="sustained window / auto --steps target")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--hard-paths", type=int, default=1, help="QEC_OPT_HARD_PATHS for the timed run")
-    ap.add_argument("--no-gather", action="store_true",
-                    help="N > 1: skip the (untimed-step) RCCL gather of bit-packed decisions to rank 0")
-    ap.add_argument("--no-full-arith", action="store_true",
-                    help="skip the full_arithmetic re-timing (profiling runs: keeps the launch average clean)")
+    ap.add_argument("--no-gather", action="store_true", help="N > 1: skip the RCCL gather measurements")
+    ap.add_argument("--no-extras", action="store_true",
+                    help="only the timed steps (profiling runs: no full-arithmetic / phase / sustained re-timings)")
     args = ap.parse_args()
 
     import torch
@@ -99,50 +130,163 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and rank == 0:
+        print("warning: --gpus %d but WORLD_SIZE %d; using WORLD_SIZE" % (args.gpus, world), file=sys.stderr)
+    backend = None
     if world > 1:
         # RCCL ("nccl") over xGMI; QEC_BENCH_BACKEND=gloo rehearses the multi-rank path with
         # several ranks sharing one GPU (RCCL needs one GPU per rank)
-        dist.init_process_group(os.environ.get("QEC_BENCH_BACKEND") or "nccl")
+        backend = os.environ.get("QEC_BENCH_BACKEND") or "nccl"
+        dist.init_process_group(backend)
     local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
-    fname, p_def, it_def, label = CODES[args.code]
+    fname, p_def, it_def = CODES[args.code]
     p = args.p if args.p is not None else p_def
     iters = args.iters if args.iters is not None else it_def
     code = q.Quantum_LDPC_Code.createFromFile(code_path(fname))
-    dec = q.DecoderGPU(code, local)
+    if args.batch is not None:
+        scaling, lo, hi = "weak", rank * args.batch, (rank + 1) * args.batch
+        global_batch = args.batch * world
+    else:
+        scaling, global_batch = "strong", args.global_batch
+        lo, hi = shard(global_batch, rank, world)
+    B = hi - lo
+    dec = q.DecoderGPU(code, local, max_batch=B)
     dec.set_option("hard_paths", args.hard_paths)
-    B = args.batch
 
-    # rank's shard of the sample index space, [rank*B, (rank+1)*B), drawn on the device
-    # (Philox depolarising sampler + circulant syndrome kernel) before the timed region
-    x = torch.empty((B, code.n), dtype=torch.uint8, device=dev)
-    z = torch.empty((B, code.n), dtype=torch.uint8, device=dev)
+    # the rank's shard of the sample index space, drawn and turned into syndromes on the device
+    # (fused Philox sampler + syndrome kernel) before the timed region
     sX = torch.empty((B, code.numEqsX), dtype=torch.uint8, device=dev)
     sZ = torch.empty((B, code.numEqsZ), dtype=torch.uint8, device=dev)
-    dec.sample_depolarizing_dev(SEED, rank * B, p, x, z)
-    dec.syndrome_dev(x, z, sX, sZ)
-    torch.cuda.synchronize(dev)
-    del x, z
-    eX = torch.empty((B, code.n), dtype=torch.uint8, device=dev)
-    eZ = torch.empty((B, code.n), dtype=torch.uint8, device=dev)
-    fl = torch.empty(B, dtype=torch.uint8, device=dev)
-    its = torch.empty((B, 2), dtype=torch.int32, device=dev)
     stream = torch.cuda.current_stream(dev)
+    dec.sample_syndrome_dev(SEED, lo, p, sX, sZ, stream=stream)
+    its = torch.empty((B, 2), dtype=torch.int32, device=dev)
+    packed = args.output == "packed"
+    if packed:
+        rec = torch.empty((B, dec.record_bytes()), dtype=torch.uint8, device=dev)
+        outs = (rec, its)
 
-    def step():
-        dec.decode_batch_dev(sX, sZ, p, iters, args.stop, eX, eZ, fl, its, stream=stream)
+        def step():
+            dec.decode_batch_packed_dev(sX, sZ, p, iters, args.stop, rec, its, stream=stream)
+    else:
+        eX = torch.empty((B, code.n), dtype=torch.uint8, device=dev)
+        eZ = torch.empty((B, code.n), dtype=torch.uint8, device=dev)
+        fl = torch.empty(B, dtype=torch.uint8, device=dev)
+        outs = (eX, eZ, fl, its)
+
+        def step():
+            dec.decode_batch_dev(sX, sZ, p, iters, args.stop, eX, eZ, fl, its, stream=stream)
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
+    steps = args.steps
+    if steps is None:  # enough steps for a >= min-seconds window (probe 3 steps)
+        t = time.perf_counter()
+        for _ in range(3):
+            step()
+        torch.cuda.synchronize(dev)
+        per = (time.perf_counter() - t) / 3
+        steps = max(5, int(math.ceil(args.min_seconds / max(per, 1e-6))))
+        if world > 1:
+            s = torch.tensor([steps], dtype=torch.int64, device=dev)
+            dist.all_reduce(s, op=dist.ReduceOp.MAX)
+            steps = int(s.item())
+
+    elapsed, kernel_ms = timed_steps(step, steps, stream, dev, world)
+    total = B * world * steps if scaling == "weak" else global_batch * steps
+    value = total / elapsed
+    ms_per_step = elapsed / steps * 1e3
+
+    # executed iterations of the timed batch (fixed: == iters)
+    it_np = its.cpu().numpy()
+    it_mean = (float(it_np[:, 0].mean()), float(it_np[:, 1].mean()))
+    workload = ("BASELINE configs[3]: J=4,K=5,L=10,P=61 code, 2^20 syndromes sharded over %d GPU(s)" % world
+                if args.code == "p61" and scaling == "strong" and global_batch == GLOBAL_BATCH else
+                "%s code, %d syndromes %s" % (code.describe(), global_batch,
+                                              "per step over %d GPU(s)" % world if scaling == "strong"
+                                              else "(%d per GPU, weak scaling)" % B))
+    stop_label = {"fixed": "%d fixed BP iters" % iters, "ref": "reference stop rule (DecoderCPU::Decode), cap %d" % iters,
+                  "syndrome": "syndrome stop, cap %d" % iters}[args.stop]
+    metric = {"fixed": "syndromes decoded/sec (fixed BP iters)",
+              "ref": "syndromes decoded/sec (reference stop rule)",
+              "syndrome": "syndromes decoded/sec (syndrome stop)"}[args.stop]
+    out = {
+        "metric": metric,
+        "value": round(value, 1),
+        "unit": "syndromes/s",
+        "n_gpus": world,
+        "steps": steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True,
+        "scaling": scaling,
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic i.i.d. depolarising errors (device Philox4x32-10 sampler, seed 0x51EC0DE), "
+                "syndromes resident in HBM",
+        "config": {"workload": workload + ", " + stop_label, "code": code.describe(), "global_batch": global_batch,
+                   "per_gpu_batch": B, "bp_iters": iters, "stop": args.stop, "p": p, "output": args.output,
+                   "parallelism": "dp%d" % world, "kernel": dec.describe()},
+        "p": p,
+        "mean_iterations": {"X": round(it_mean[0], 4), "Z": round(it_mean[1], 4)},
+        "decode_ms": round(kernel_ms, 4),
+    }
+    pm, pm_path = load_pmc(args.code, iters, args.stop, p)
+    out["roofline"] = valu_roofline(pm, pm_path, B, kernel_ms, args.hard_paths)
+    ab = algorithmic_bytes_per_syndrome(code, it_mean[0], it_mean[1]) * B
+    gbs = ab / (kernel_ms * 1e-3) / 1e9
+    out["roofline_hbm_alg"] = {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                               "frac": round(gbs / HBM_PEAK_GBS, 4), "valid": gbs <= HBM_PEAK_GBS,
+                               "algorithmic_bytes_per_launch": int(ab),
+                               "note": "SURVEY 8(d) HBM-resident flooding schedule; the engine keeps messages in "
+                                       "VGPRs, so this is not its bound when frac > 1"}
+
+    if not args.no_extras:
+        if args.hard_paths:
+            full = retime(dec, step, stream, B, outs, {"hard_paths": 0})
+            out["value_full_arithmetic"] = round(full["syndromes_per_s"] * (world if scaling == "weak" else 1)
+                                                 * (global_batch / (B * world) if scaling == "strong" else 1), 1)
+            ops = lane_ops_per_syndrome(code, 1) * (it_mean[0] + it_mean[1]) / 2.0
+            tops = ops * B / (full["kernel_ms"] * 1e-3) / 1e12
+            full["valu_lane_ops"] = {"achieved": round(tops, 2), "peak": VALU_PEAK_TOPS, "unit": "Tlane-op/s",
+                                     "frac": round(tops / VALU_PEAK_TOPS, 4),
+                                     "basis": "analytical lane-ops of full-arithmetic BP (DESIGN.md section 5)"}
+            out["full_arithmetic"] = full
+            out["no_cycle_jump"] = retime(dec, step, stream, B, outs, {"cycle_jump": 0})
+        out["sector_iterations"] = phase_counts(dec, step, stream, its, B)
+        out["sustained"] = sustained(step, stream, dev, world, ms_per_step, args.min_seconds,
+                                     global_batch if scaling == "strong" else B * world)
+
+    if world > 1 and not args.no_gather and packed:
+        try:
+            out["gather"] = gather_measure(dec, step, rec, B, world, rank, dev, stream, steps, global_batch, backend)
+        except Exception as exc:  # noqa: BLE001 -- a failure here must not cost the bench line
+            out["gather"] = {"error": "%s: %s" % (type(exc).__name__, exc)}
+
+    if rank == 0 and world == 1 and not args.no_cpu:
+        out["cpu_baseline"] = cpu_baseline(code, fname, sX, sZ, p, iters, args, outs, packed)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+
+
+def timed_steps(step, steps, stream, dev, world):
+    """K steps between barrier + synchronize on both sides; wall time max over ranks, and the
+    mean decode-launch time from HIP events on the launch stream."""
+    import torch
+    import torch.distributed as dist
+    torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
     t0 = time.perf_counter()
-    for k in range(args.steps):
+    for k in range(steps):
         ev[k][0].record(stream)
         step()
         ev[k][1].record(stream)
@@ -156,128 +300,37 @@ def main():
         t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kernel_ms = float(t[0]), float(t[1])
-
-    total = B * world * args.steps
-    value = total / elapsed
-    ms_per_step = elapsed / args.steps * 1e3
-
-    # executed iterations (fixed: == iters); mean over the batch for the other rules
-    it_np = its.cpu().numpy()
-    it_mean = (float(it_np[:, 0].mean()), float(it_np[:, 1].mean()))
-    EX, EZ = code.numEqsX * code.L, code.numEqsZ * code.L
-    io = -(-(code.numEqsX + code.numEqsZ) // 8) + -(-(2 * code.n) // 8) + 1
-    bytes_per_syn = 16 * (EX * it_mean[0] + EZ * it_mean[1]) + io
-    achieved_gbs = bytes_per_syn * B / (kernel_ms * 1e-3) / 1e9
-    ops = lane_ops_per_syndrome(code, 1) * (it_mean[0] + it_mean[1]) / 2.0
-    full = None
-    nojump = None
-    if args.hard_paths and not args.no_full_arith:
-        full = full_arithmetic(dec, step, stream, B, (eX, eZ, fl, its))
-        nojump = full_arithmetic(dec, step, stream, B, (eX, eZ, fl, its), option="cycle_jump")
-    # the analytical count is the full-arithmetic work: only a launch without the
-    # hard-message paths can be priced against it
-    valu_ms = full["kernel_ms"] if full else (kernel_ms if not args.hard_paths else None)
-    achieved_tops = ops * B / (valu_ms * 1e-3) / 1e12 if valu_ms else None
-    traffic = None
-    prof = os.path.join(ROOT, "profiles", "pmc_%s.json" % args.code)
-    if os.path.exists(prof):
-        try:
-            with open(prof) as f:
-                pm = json.load(f)
-            if pm.get("batch") == B and pm.get("iters") == iters and pm.get("stop") == args.stop:
-                traffic = pm.get("hbm_bytes_per_launch")
-        except (ValueError, OSError):
-            traffic = None
-
-    out = {
-        "metric": "syndromes decoded/sec (fixed BP iters)",
-        "value": round(value, 1),
-        "unit": "syndromes/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": round(ms_per_step, 4),
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "f32",
-        "data": "synthetic i.i.d. depolarising errors (device Philox4x32-10 sampler, seed 0x51EC0DE), "
-                "syndromes resident in HBM",
-        "config": {"workload": label if world == 1 else label + " (BASELINE configs[3] shape, sharded)",
-                   "code": code.describe(), "global_batch": B * world, "per_gpu_batch": B,
-                   "bp_iters": iters, "stop": args.stop, "p": p, "parallelism": "dp%d" % world,
-                   "kernel": dec.describe()},
-        "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved_gbs / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "algorithmic_bytes_per_launch": int(bytes_per_syn * B), "kernel_ms": round(kernel_ms, 4)},
-        "valu": None if achieved_tops is None else
-                {"achieved": round(achieved_tops, 2), "peak": VALU_PEAK_TOPS, "unit": "Tlane-op/s",
-                 "frac": round(achieved_tops / VALU_PEAK_TOPS, 4), "kernel_ms": round(valu_ms, 4),
-                 "launch": "full_arithmetic" if full else "timed (hard paths off)"},
-    }
-    if full:
-        out["full_arithmetic"] = full
-        out["no_cycle_jump"] = nojump
-    if args.stop != "fixed":
-        hist = np.bincount(it_np.ravel(), minlength=iters + 1)
-        out["iteration_histogram"] = {str(k): int(v) for k, v in enumerate(hist) if v}
-
-    if world > 1 and not args.no_gather:
-        # measured after the timed steps; a failure here must not cost the bench line
-        try:
-            out["gather"] = gather_step(dec, eX, eZ, fl, B, world, rank, dev, stream)
-        except Exception as exc:  # noqa: BLE001
-            out["gather"] = {"error": "%s: %s" % (type(exc).__name__, exc)}
-
-    if rank == 0 and world == 1 and not args.no_cpu:
-        out["cpu_baseline"] = cpu_baseline(code, fname, sX.cpu().numpy(), sZ.cpu().numpy(), p, iters, args, eX, eZ, fl)
-    if world > 1:
-        dist.barrier()
-        dist.destroy_process_group()
-    if rank == 0:
-        print(json.dumps(out), flush=True)
+    return elapsed, kernel_ms
 
 
-def gather_step(dec, eX, eZ, fl, B, world, rank, dev, stream):
-    """every rank bit-packs its decoded shard on the device and the records
-    are gathered to rank 0 over RCCL.  Measured after (not inside) the timed decode steps:
-    the decode itself needs no exchange."""
-    import torch
-    import torch.distributed as dist
-    from qec_ldpc_amd.gather import gather_records
-    rec = torch.empty((B, dec.record_bytes()), dtype=torch.uint8, device=dev)
-    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    a.record(stream)
-    dec.pack_decisions_dev(eX, eZ, fl, rec, stream=stream)
-    b.record(stream)
-    torch.cuda.synchronize(dev)
-    pack_ms = a.elapsed_time(b)
-    gather_records(rec)  # warm-up (communicator set-up)
-    torch.cuda.synchronize(dev)
-    dist.barrier()
-    t0 = time.perf_counter()
-    full = gather_records(rec)
-    torch.cuda.synchronize(dev)
-    dist.barrier()
-    ms = (time.perf_counter() - t0) * 1e3
-    t = torch.tensor([ms, pack_ms], dtype=torch.float64, device=dev)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    ok = True
-    if rank == 0:
-        ok = bool(torch.equal(full[:B], rec))
-    nbytes = B * rec.shape[1]
-    return {"record_bytes": int(rec.shape[1]), "bytes_per_rank": int(nbytes), "pack_ms": round(float(t[1]), 4),
-            "gather_ms": round(float(t[0]), 4), "root_GBps": round(world * nbytes / (float(t[0]) * 1e-3) / 1e9, 2),
-            "rank0_shard_intact": ok}
+def valu_roofline(pm, path, B, kernel_ms, hard_paths):
+    """VALU-issue roofline of the decode kernel: PMC SQ_INSTS_VALU (wave instructions) per
+    syndrome x B, each taking VALU_ISSUE_CYCLES of a SIMD, over this run's launch time."""
+    peak = SIMDS * CLOCK_GHZ * 1e9 / VALU_ISSUE_CYCLES / 1e12  # T wave-instructions/s
+    base = {"bound": "valu", "peak": round(peak, 4), "unit": "Twave-instr/s",
+            "peak_basis": "1024 SIMDs x 2.4 GHz / 2 cycles per wave64 VALU instruction"}
+    if pm is None or "valu_insts_per_syndrome" not in pm or not hard_paths:
+        base.update({"achieved": None, "frac": None, "traffic": None,
+                     "note": "no PMC profile for this workload (%s)" % os.path.relpath(path, ROOT)})
+        return base
+    insts = pm["valu_insts_per_syndrome"] * B
+    ach = insts / (kernel_ms * 1e-3) / 1e12
+    base.update({"achieved": round(ach, 4), "frac": round(ach / peak, 4),
+                 "traffic": int(round(pm["hbm_bytes_per_syndrome"] * B)) if pm.get("hbm_bytes_per_syndrome") else None,
+                 "valu_insts_per_launch": int(insts), "kernel_ms": round(kernel_ms, 4),
+                 "profile": os.path.relpath(path, ROOT), "profile_batch": pm.get("batch"),
+                 "profile_frac": pm.get("valu_issue_frac")})
+    return base
 
 
-def full_arithmetic(dec, step, stream, B, outs, reps=3, option="hard_paths"):
-    """Re-time the step with a shortcut option off (hard_paths: every iteration in full
-    arithmetic; cycle_jump: hard iterations run one by one) and check the outputs are the
-    same bits."""
+def retime(dec, step, stream, B, outs, opts, reps=3):
+    """Re-time the step with decoder options changed (e.g. hard_paths 0: every iteration in full
+    arithmetic) and check the outputs are the same bits."""
     import torch
     ref = [t.clone() for t in outs]
-    dec.set_option(option, 0)
+    old = {k: dec.get_option(k) for k in opts}
+    for k, v in opts.items():
+        dec.set_option(k, v)
     try:
         step()
         ms = []
@@ -289,29 +342,129 @@ def full_arithmetic(dec, step, stream, B, outs, reps=3, option="hard_paths"):
             torch.cuda.synchronize()
             ms.append(a.elapsed_time(b))
     finally:
-        dec.set_option(option, 1)
+        for k, v in old.items():
+            dec.set_option(k, v)
     same = all(torch.equal(r, t) for r, t in zip(ref, outs))
     k = float(np.median(ms))
     return {"kernel_ms": round(k, 4), "syndromes_per_s": round(B / k * 1e3, 1), "identical": bool(same)}
 
 
-def cpu_baseline(code, fname, sX_h, sZ_h, p, iters, args, eX, eZ, fl):
-    """Oracle (CPU restatement of DecoderCPU, one decoder per OpenMP thread) on a bounded
-    sample of the same batch; also checks the GPU's answers on that sample."""
+def phase_counts(dec, step, stream, its, B):
+    """One launch of the instrumented kernel (QEC_OPT_PHASE_STATS): iters[] then packs, per
+    sector, soft | hard << 8 | agreed << 16 | jumped << 24 iterations."""
+    import torch
+    try:
+        dec.set_option("phase_stats", 1)
+    except Exception as exc:  # noqa: BLE001
+        return {"error": str(exc)}
+    try:
+        step()
+        torch.cuda.synchronize()
+        v = its.cpu().numpy().astype(np.int64)
+    finally:
+        dec.set_option("phase_stats", 0)
+    out = {}
+    for name, shift in (("soft", 0), ("hard", 8), ("agreed", 16), ("jumped", 24)):
+        c = (v >> shift) & 0xFF
+        out[name] = {"X": int(c[:, 0].sum()), "Z": int(c[:, 1].sum())}
+    executed = sum(out[k]["X"] + out[k]["Z"] for k in ("soft", "hard", "agreed"))
+    out["per_launch"] = {"syndromes": B, "sector_iterations_executed": executed,
+                         "sector_iterations_nominal": executed + out["jumped"]["X"] + out["jumped"]["Z"]}
+    step()  # restore the timed outputs
+    torch.cuda.synchronize()
+    return out
+
+
+def sustained(step, stream, dev, world, ms_per_step, min_seconds, per_step_units):
+    n = max(5, int(math.ceil(min_seconds * 1e3 / max(ms_per_step, 1e-3))))
+    elapsed, _ = timed_steps(step, n, stream, dev, world)
+    return {"steps": n, "seconds": round(elapsed, 3), "syndromes_per_s": round(per_step_units * n / elapsed, 1)}
+
+
+def gather_measure(dec, step, rec, B, world, rank, dev, stream, steps, global_batch, backend):
+    """every rank's decision records (decoded straight into bit-packed form) are
+    gathered to rank 0.  Timed alone, and end to end (decode + gather each step)."""
+    import torch
+    import torch.distributed as dist
+    from qec_ldpc_amd.gather import gather_records
+    gather_records(rec)  # warm-up (communicator set-up)
+    torch.cuda.synchronize(dev)
+
+    def timed(fn, n):
+        dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(n):
+            fn()
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        return (time.perf_counter() - t0) / n
+
+    g = timed(lambda: gather_records(rec), max(3, min(steps, 20)))
+
+    def e2e():
+        step()
+        gather_records(rec)
+
+    e = timed(e2e, steps)
+    full = gather_records(rec)
+    ok = True
+    if rank == 0:
+        ok = bool(torch.equal(full[:B], rec))
+    t = torch.tensor([g, e], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    g, e = float(t[0]), float(t[1])
+    nbytes = B * rec.shape[1]
+    return {"backend": backend, "record_bytes": int(rec.shape[1]), "bytes_per_rank": int(nbytes),
+            "gather_ms": round(g * 1e3, 4), "root_GBps": round(world * nbytes / g / 1e9, 2),
+            "end_to_end": {"ms_per_step": round(e * 1e3, 4), "syndromes_per_s": round(global_batch / e, 1),
+                           "what": "packed decode of every shard + RCCL gather of all records to rank 0"},
+            "rank0_shard_intact": ok}
+
+
+def cpu_baseline(code, fname, sX, sZ, p, iters, args, outs, packed):
+    """Oracle (CPU restatement of DecoderCPU, one decoder per OpenMP thread) on a bounded sample of
+    the same batch, all host threads and 1 thread; checks the GPU's answers on that sample; and
+    BASELINE configs[0] (P7, 1k depolarising syndromes, 20 iterations) on all threads."""
     from oracle.oracle import OracleCode
-    from qec_ldpc_amd.codes import code_path
+    from qec_ldpc_amd.codes import P7, code_path
+    from qec_ldpc_amd.gather import unpack_records
+    import qec_ldpc_amd as q
+    from qec_ldpc_amd.synthetic import depolarizing_errors
     threads = int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)
     orc = OracleCode(code_path(fname))
-    probe = min(64 * threads, len(sX_h))
-    t = time.perf_counter()
-    orc.decode_batch(sX_h[:probe], sZ_h[:probe], p, iters, args.stop, nthreads=threads)
-    rate = probe / max(time.perf_counter() - t, 1e-9)
-    n = int(min(len(sX_h), max(probe, rate * args.cpu_seconds)))
-    t = time.perf_counter()
-    o = orc.decode_batch(sX_h[:n], sZ_h[:n], p, iters, args.stop, nthreads=threads)
-    dt = time.perf_counter() - t
-    same = (np.array_equal(o[0], eX[:n].cpu().numpy()) and np.array_equal(o[1], eZ[:n].cpu().numpy())
-            and np.array_equal(o[2], fl[:n].cpu().numpy()))
+    sX_h, sZ_h = sX.cpu().numpy(), sZ.cpu().numpy()
+
+    def rate(nthreads, seconds, cap):
+        probe = min(8 * nthreads, cap)
+        t = time.perf_counter()
+        orc.decode_batch(sX_h[:probe], sZ_h[:probe], p, iters, args.stop, nthreads=nthreads)
+        r = probe / max(time.perf_counter() - t, 1e-9)
+        n = int(min(cap, max(probe, r * seconds)))
+        t = time.perf_counter()
+        o = orc.decode_batch(sX_h[:n], sZ_h[:n], p, iters, args.stop, nthreads=nthreads)
+        return n, time.perf_counter() - t, o
+
+    n, dt, o = rate(threads, args.cpu_seconds, len(sX_h))
+    if packed:
+        gX, gZ, gF = unpack_records(outs[0][:n].cpu().numpy(), code.n)
+    else:
+        gX, gZ, gF = (t[:n].cpu().numpy() for t in outs[:3])
+    same = np.array_equal(o[0], gX) and np.array_equal(o[1], gZ) and np.array_equal(o[2], gF)
+    n1, dt1, _ = rate(1, max(2.0, args.cpu_seconds / 4), len(sX_h))
+    # BASELINE configs[0]: P7, 1k depolarising syndromes (p = 0.02), 20 iterations, all threads
+    c7 = q.Quantum_LDPC_Code.createFromFile(code_path(P7))
+    x7, z7 = depolarizing_errors(c7.n, 0, 1000, 0.02)
+    o7 = OracleCode(code_path(P7))
+    s7 = (c7.syndrome(0, x7), c7.syndrome(1, z7))
+    cfg0 = {}
+    for stop in ("fixed", "ref"):
+        t = time.perf_counter()
+        reps = 0
+        while time.perf_counter() - t < 1.0 or reps < 3:
+            o7.decode_batch(s7[0], s7[1], 0.02, 20, stop, nthreads=threads)
+            reps += 1
+        cfg0[stop] = round(1000 * reps / (time.perf_counter() - t), 1)
     cpu_model = ""
     try:
         for line in open("/proc/cpuinfo"):
@@ -322,7 +475,10 @@ def cpu_baseline(code, fname, sX_h, sZ_h, p, iters, args, eX, eZ, fl):
         pass
     return {"value": round(n / dt, 2), "unit": "syndromes/s", "cores": threads, "kind": "port",
             "sample": "first %d syndromes of rank 0's batch, %s stop, %d iters (%.1f s)" % (n, args.stop, iters, dt),
-            "cpu": cpu_model, "gpu_matches_oracle_on_sample": bool(same)}
+            "cpu": cpu_model, "gpu_matches_oracle_on_sample": bool(same),
+            "one_thread": {"value": round(n1 / dt1, 2), "sample": "first %d syndromes (%.1f s)" % (n1, dt1)},
+            "configs0_p7_1k_20iters": {"fixed": cfg0["fixed"], "ref": cfg0["ref"], "unit": "syndromes/s",
+                                       "cores": threads, "p": 0.02}}
 
 
 if __name__ == "__main__":

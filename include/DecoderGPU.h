@@ -3,8 +3,11 @@
 // constructor and method signatures, so QEC_LDPC/main.cu's loop switches engines by
 // replacing `DecoderCPU decoder(code);` with `DecoderGPU decoder(code);`.
 //
-// Added: DecodeBatch (the batched boundary the GPU engine is built for).
-// Decode() keeps the reference's one-syndrome-pair semantics (a batch of one).
+// Added: DecodeBatch / DecodeBatchPacked (the batched boundary the GPU engine is built for), and
+// a multi-device constructor: DecoderGPU(code, {0, 1, ..., 7}) spreads GetStatistics' samples
+// (and batched decodes) over the listed GPUs with counters identical to one device
+// (qec_decoder_create_multi).  Decode() keeps the reference's one-syndrome-pair semantics (a
+// batch of one: one launch, copies and a synchronisation per call -- loop DecodeBatch instead).
 #pragma once
 #include <cstdint>
 #include <random>
@@ -20,6 +23,12 @@ public:
     explicit DecoderGPU(Quantum_LDPC_Code code, int device = 0) : Decoder(code)
     {
         dec_ = qec_decoder_create(_code.handle(), device, 0);
+        if (!dec_) throw std::string(qec_last_error());
+    }
+    // several GPUs of this node (a device may repeat); every call shards its samples over them
+    DecoderGPU(Quantum_LDPC_Code code, const std::vector<int>& devices) : Decoder(code)
+    {
+        dec_ = qec_decoder_create_multi(_code.handle(), devices.data(), (int)devices.size(), 0);
         if (!dec_) throw std::string(qec_last_error());
     }
     ~DecoderGPU() override { qec_decoder_destroy(dec_); }
@@ -50,6 +59,15 @@ public:
         flags.resize(B);
         check(qec_decode_batch(dec_, sX.data(), sZ.data(), B, errorProbability, maxIterations, stopRule, eX.data(),
                                eZ.data(), flags.data(), nullptr, nullptr));
+    }
+
+    // B syndrome pairs -> packed decision records [B * QEC_RECORD_BYTES(n)] (eX bits, eZ bits, flags)
+    void DecodeBatchPacked(const std::vector<uint8_t>& sX, const std::vector<uint8_t>& sZ, size_t B,
+                           float errorProbability, int maxIterations, int stopRule, std::vector<uint8_t>& records)
+    {
+        records.resize(B * QEC_RECORD_BYTES(_code.n));
+        check(qec_decode_batch_packed(dec_, sX.data(), sZ.data(), B, errorProbability, maxIterations, stopRule,
+                                      records.data(), nullptr));
     }
 
     // DecoderGPU::GetStats (DecoderGPU.h:193-228): statistics over pre-generated flat

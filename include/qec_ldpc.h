@@ -13,6 +13,13 @@
  * one qec_decoder are serialised by the caller (like one DecoderCPU per OpenMP
  * thread, QEC_LDPC/DecoderCPU.h:431); distinct decoders may be driven from
  * distinct host threads.
+ *
+ * Streams: the device-pointer (_dev) entry points enqueue on the caller's stream and
+ * return without synchronising.  A decoder's workspace (dispatch order, flag-merge
+ * words) is reused by every launch; a launch on a stream other than the previous
+ * launch's first waits for that launch (an event), so calls on one decoder from
+ * several streams are ordered, not concurrent.  For concurrency use one decoder per
+ * stream.  Every entry point restores the caller's current HIP device.
  */
 #ifndef QEC_LDPC_H
 #define QEC_LDPC_H
@@ -24,7 +31,7 @@
 extern "C" {
 #endif
 
-#define QEC_LDPC_ABI_VERSION 3
+#define QEC_LDPC_ABI_VERSION 4
 
 /* status codes */
 enum {
@@ -113,8 +120,10 @@ int qec_code_check_logical(const qec_code* code, const uint8_t* ex, const uint8_
 
 /* ---- decoder (DecoderGPU, QEC_LDPC/DecoderGPU.h:11-281) ------------------- */
 /* Replaces DecoderGPU(Quantum_LDPC_Code) (DecoderGPU.h:117-130).  device = HIP
- * device ordinal (>= 0; there is no CPU engine in the product).  max_batch sizes
- * the host-pointer staging buffers (grown on demand). */
+ * device ordinal (>= 0; there is no CPU engine in the product).  max_batch sizes the
+ * device-pointer workspace up front: the _dev decode entry points then allocate nothing
+ * for B <= max_batch and may be captured into a graph.  Larger batches grow it on
+ * demand (an error while the stream is being captured). */
 qec_decoder* qec_decoder_create(const qec_code* code, int device, size_t max_batch);
 /* Same with an explicit engine (QEC_ENGINE_*).  QEC_ENGINE_CIRCULANT fails with
  * QEC_ERR_UNSUPPORTED when the code has no wave-circulant kernel; QEC_ENGINE_SPARSE fails
@@ -122,6 +131,18 @@ qec_decoder* qec_decoder_create(const qec_code* code, int device, size_t max_bat
  * J / K, DecoderCPU.h:41-84). */
 qec_decoder* qec_decoder_create_engine(const qec_code* code, int device, size_t max_batch, int engine);
 int qec_decoder_destroy(qec_decoder* dec);
+/* A decoder over several devices (the reference's sample-parallel loop, DecoderCPU.h:419-438,
+ * spread over GPUs; main.cu:79,101 unchanged): one single-device part per entry of devices[]
+ * (a device may appear more than once: two parts then share it).  The host-pointer entry
+ * points (qec_decode_batch, qec_decode_batch_packed) split the batch into contiguous shards,
+ * one per part, decoded concurrently; qec_get_statistics and qec_monte_carlo shard their
+ * samples the same way and sum the parts' counters (bit-identical to one device: the counters
+ * do not depend on sample order).  Options apply to every part.  The _dev entry points need
+ * a single-device handle: call them on qec_decoder_part(dec, k). */
+qec_decoder* qec_decoder_create_multi(const qec_code* code, const int* devices, int ndevices, size_t max_batch);
+int qec_decoder_num_parts(const qec_decoder* dec);      /* 1 for a single-device decoder */
+qec_decoder* qec_decoder_part(qec_decoder* dec, int k); /* part k (the handle itself for k = 0 of a single one) */
+int qec_decoder_device(const qec_decoder* dec);         /* HIP device ordinal (of part 0 for a group) */
 /* Decoder options (no reference analogue: DecoderCPU has none).
  *   QEC_OPT_HARD_PATHS (default 1): once every message of a sector is exactly +0 or 1.0 the
  *     wave-circulant kernels switch to the exact hard-message forms of the check and variable
@@ -144,8 +165,14 @@ int qec_decoder_destroy(qec_decoder* dec);
  *     waves instead of one after the other (halves the longest wave).  The launch then zeroes
  *     flags[] first and each sector ORs in its bits.  Bit-identical either way.  0 = off,
  *     1 = the kernel variant's measured choice (on for P7, off for P61), 2 = on where the
- *     variant has split kernels (the two shipped codes). */
-enum { QEC_OPT_HARD_PATHS = 1, QEC_OPT_CYCLE_JUMP = 2, QEC_OPT_SCHEDULE = 3, QEC_OPT_SECTOR_SPLIT = 4 };
+ *     variant has split kernels (the two shipped codes).
+ *   QEC_OPT_PHASE_STATS (default 0; measurement only, shipped codes): launches an instrumented
+ *     copy of the kernel whose iters[] output packs, per sector, the iterations executed in each
+ *     phase instead of their count: soft | hard << 8 | agreed << 16 | jumped << 24 (soft: full
+ *     arithmetic; hard: hard-message forms; agreed: the agreement path; jumped: skipped by the
+ *     cycle jump; each field mod 256).  Decisions and flags are unchanged. */
+enum { QEC_OPT_HARD_PATHS = 1, QEC_OPT_CYCLE_JUMP = 2, QEC_OPT_SCHEDULE = 3, QEC_OPT_SECTOR_SPLIT = 4,
+       QEC_OPT_PHASE_STATS = 5 };
 int qec_decoder_set_option(qec_decoder* dec, int option, int value);
 int qec_decoder_get_option(const qec_decoder* dec, int option, int* value);
 /* which kernel variant serves this code: writes a short name (e.g. "wave-circulant P=61 G=1") */
@@ -169,6 +196,18 @@ int qec_decode_batch_dev(qec_decoder* dec, const uint8_t* sX, const uint8_t* sZ,
                          float errorProbability, int maxIterations, int stop,
                          uint8_t* eX, uint8_t* eZ, uint8_t* flags, int32_t* iters, float* q_final,
                          void* stream);
+/* Bit-packed output (SURVEY.md 8(d)'s I/O model): the decode kernel writes one decision record
+ * per syndrome instead of eX / eZ / flags: records is B x QEC_RECORD_BYTES(n) bytes, per syndrome
+ * eX packed (ceil(n/8) bytes, bit j of byte k = qubit 8k + j, padding bits 0), then eZ packed,
+ * then the ErrorCode flags byte.  Same decisions bit for bit as the byte form. */
+#define QEC_RECORD_BYTES(n) (2 * (((n) + 7) / 8) + 1)
+int qec_decode_batch_packed_dev(qec_decoder* dec, const uint8_t* sX, const uint8_t* sZ, size_t B,
+                                float errorProbability, int maxIterations, int stop,
+                                uint8_t* records, int32_t* iters, float* q_final, void* stream);
+/* Host-buffer form of the packed decode (synchronous). */
+int qec_decode_batch_packed(qec_decoder* dec, const uint8_t* sX, const uint8_t* sZ, size_t B,
+                            float errorProbability, int maxIterations, int stop,
+                            uint8_t* records, int32_t* iters);
 
 /* ---- Monte-Carlo caller side (DecoderCPU::GetStatistics, DecoderCPU.h:392-530) */
 /* The reference's fixed-weight sampler (DecoderCPU.h:448-459, RandomErrorGenerator.h:31-44):
@@ -185,7 +224,9 @@ int qec_get_statistics(qec_decoder* dec, int errorWeight, int numErrors, float e
 /* ---- Monte-Carlo on the device (the GetStatistics loop, batched) ---- */
 /* counters in device order for qec_statistics_dev */
 enum { QEC_MC_WITHX, QEC_MC_WITHZ, QEC_MC_SYNX, QEC_MC_SYNZ, QEC_MC_LOGICAL, QEC_MC_CORRECTED, QEC_MC_CONVX,
-       QEC_MC_CONVZ, QEC_MC_NCOUNTERS };
+       QEC_MC_CONVZ, QEC_MC_NCOUNTERS,
+       /* qec_statistics_packed_dev with iters: BP iterations executed, summed per sector */
+       QEC_MC_ITERX = QEC_MC_NCOUNTERS, QEC_MC_ITERZ, QEC_MC_NCOUNTERS_ALL };
 
 typedef struct {
     uint64_t tested, withX, withZ, synX, synZ, logical, corrected, convX, convZ;
@@ -200,6 +241,13 @@ typedef struct {
  * (0 = X, 1 = Y, 2 = Z; Y sets both bits).  Any shard of the index space can be drawn alone. */
 int qec_sample_depolarizing_dev(qec_decoder* dec, uint64_t seed, uint64_t start, size_t B, float p, uint8_t* x,
                                 uint8_t* z, void* stream);
+/* Fused front end: the depolarising errors of qec_sample_depolarizing_dev (same stream, same
+ * bits) go straight to their syndromes (GetSyndromeX/Z, Quantum_LDPC_Code.h:94-124) without
+ * leaving the chip: sX B x numEqsX, sZ B x numEqsZ, and optionally errp B x 2 ceil(n/8), the
+ * errors bit-packed in the decision-record layout (x bits then z bits) for
+ * qec_statistics_packed_dev.  One wave per sample. */
+int qec_sample_syndrome_dev(qec_decoder* dec, uint64_t seed, uint64_t start, size_t B, float p, uint8_t* sX,
+                            uint8_t* sZ, uint8_t* errp, void* stream);
 /* GetSyndromeX/Z (Quantum_LDPC_Code.h:94-124) of device error vectors: x, z B x n -> sX B x numEqsX, sZ B x numEqsZ */
 int qec_syndrome_dev(qec_decoder* dec, const uint8_t* x, const uint8_t* z, size_t B, uint8_t* sX, uint8_t* sZ,
                      void* stream);
@@ -208,6 +256,11 @@ int qec_syndrome_dev(qec_decoder* dec, const uint8_t* x, const uint8_t* z, size_
  * the device array counters[QEC_MC_NCOUNTERS] (uint64). */
 int qec_statistics_dev(qec_decoder* dec, const uint8_t* x, const uint8_t* z, const uint8_t* eX, const uint8_t* eZ,
                        const uint8_t* flags, size_t B, uint64_t* counters, void* stream);
+/* The same counters from packed errors (qec_sample_syndrome_dev's errp) and packed decision
+ * records (qec_decode_batch_packed_dev), ADDED to counters[QEC_MC_NCOUNTERS], or, with iters
+ * (B x 2, nullable) given, to counters[QEC_MC_NCOUNTERS_ALL] including the iteration sums. */
+int qec_statistics_packed_dev(qec_decoder* dec, const uint8_t* errp, const uint8_t* records, const int32_t* iters,
+                              size_t B, uint64_t* counters, void* stream);
 /* Decision records for gathering a sharded batch to one rank (the decoded
  * vectors travel bit-packed): out is B x (2 ceil(n/8) + 1) bytes, per syndrome eX packed
  * (bit j of byte k = qubit 8k + j), then eZ packed, then the ErrorCode flags byte.  Device
@@ -215,8 +268,10 @@ int qec_statistics_dev(qec_decoder* dec, const uint8_t* x, const uint8_t* z, con
 int qec_pack_decisions_dev(qec_decoder* dec, const uint8_t* eX, const uint8_t* eZ, const uint8_t* flags, size_t B,
                            uint8_t* out, void* stream);
 /* A whole Monte-Carlo run on the device: `count` depolarising samples from `start` of stream
- * `seed`, in batches of `batch`: sample -> syndrome -> decode (stop rule `stop`) -> statistics.
- * Synchronous; fills *out. */
+ * `seed`, in batches of `batch`: fused sample + syndrome -> packed decode (stop rule `stop`) ->
+ * statistics with iteration sums, all on the device with no per-batch host synchronisation.
+ * A multi-device decoder shards [start, start + count) contiguously over its parts.
+ * Synchronous; fills *out (decodeSeconds: decode-kernel time, the largest over parts). */
 int qec_monte_carlo(qec_decoder* dec, uint64_t seed, uint64_t start, uint64_t count, float errorProbability,
                     int maxIterations, int stop, size_t batch, qec_mc_result* out);
 

@@ -26,21 +26,29 @@ CONVERGENCE_FAIL_X = 4
 CONVERGENCE_FAIL_Z = 8
 STOP = {"ref": 0, "fixed": 1, "syndrome": 2}
 ENGINE = {"auto": 0, "circulant": 1, "sparse": 2}
-OPTION = {"hard_paths": 1, "cycle_jump": 2, "schedule": 3, "sector_split": 4}
+OPTION = {"hard_paths": 1, "cycle_jump": 2, "schedule": 3, "sector_split": 4, "phase_stats": 5}
 
 # every symbol include/qec_ldpc.h declares
 EXPORTS = (
     "qec_last_error", "qec_abi_version",
     "qec_code_load", "qec_code_generate", "qec_code_free", "qec_code_params", "qec_code_exponents",
     "qec_code_pcm", "qec_code_describe", "qec_code_syndrome", "qec_code_check_logical",
-    "qec_decoder_create", "qec_decoder_create_engine", "qec_decoder_destroy", "qec_decoder_describe",
+    "qec_decoder_create", "qec_decoder_create_engine", "qec_decoder_create_multi", "qec_decoder_destroy",
+    "qec_decoder_num_parts", "qec_decoder_part", "qec_decoder_device", "qec_decoder_describe",
     "qec_decoder_set_option", "qec_decoder_get_option",
-    "qec_decode_batch", "qec_decode_batch_dev",
+    "qec_decode_batch", "qec_decode_batch_dev", "qec_decode_batch_packed", "qec_decode_batch_packed_dev",
     "qec_sample_fixed_weight", "qec_get_statistics",
-    "qec_sample_depolarizing_dev", "qec_syndrome_dev", "qec_statistics_dev", "qec_pack_decisions_dev",
+    "qec_sample_depolarizing_dev", "qec_sample_syndrome_dev", "qec_syndrome_dev", "qec_statistics_dev",
+    "qec_statistics_packed_dev", "qec_pack_decisions_dev",
     "qec_monte_carlo",
 )
 MC_COUNTERS = ("withX", "withZ", "synX", "synZ", "logical", "corrected", "convX", "convZ")
+MC_COUNTERS_ALL = MC_COUNTERS + ("iterationsX", "iterationsZ")
+
+
+def record_bytes(n):
+    """Bytes of one packed decision record (QEC_RECORD_BYTES): eX bits, eZ bits, flags byte."""
+    return 2 * ((n + 7) // 8) + 1
 
 
 class QecError(RuntimeError):
@@ -103,17 +111,25 @@ def lib():
             "qec_code_check_logical": (i, [vp, vp, vp, sz, vp]),
             "qec_decoder_create": (vp, [vp, i, sz]),
             "qec_decoder_create_engine": (vp, [vp, i, sz, i]),
+            "qec_decoder_create_multi": (vp, [vp, vp, i, sz]),
             "qec_decoder_destroy": (i, [vp]),
+            "qec_decoder_num_parts": (i, [vp]),
+            "qec_decoder_part": (vp, [vp, i]),
+            "qec_decoder_device": (i, [vp]),
             "qec_decoder_describe": (i, [vp, ctypes.c_char_p, sz]),
             "qec_decoder_set_option": (i, [vp, i, i]),
             "qec_decoder_get_option": (i, [vp, i, vp]),
             "qec_decode_batch": (i, [vp, vp, vp, sz, f, i, i, vp, vp, vp, vp, vp]),
             "qec_decode_batch_dev": (i, [vp, vp, vp, sz, f, i, i, vp, vp, vp, vp, vp, vp]),
+            "qec_decode_batch_packed": (i, [vp, vp, vp, sz, f, i, i, vp, vp]),
+            "qec_decode_batch_packed_dev": (i, [vp, vp, vp, sz, f, i, i, vp, vp, vp, vp]),
             "qec_sample_fixed_weight": (i, [ctypes.c_uint32, i, sz, i, vp, vp]),
             "qec_get_statistics": (i, [vp, i, i, f, i, ctypes.c_uint32, i, ctypes.POINTER(Stats)]),
             "qec_sample_depolarizing_dev": (i, [vp, ctypes.c_uint64, ctypes.c_uint64, sz, f, vp, vp, vp]),
+            "qec_sample_syndrome_dev": (i, [vp, ctypes.c_uint64, ctypes.c_uint64, sz, f, vp, vp, vp, vp]),
             "qec_syndrome_dev": (i, [vp, vp, vp, sz, vp, vp, vp]),
             "qec_statistics_dev": (i, [vp, vp, vp, vp, vp, vp, sz, vp, vp]),
+            "qec_statistics_packed_dev": (i, [vp, vp, vp, vp, sz, vp, vp]),
             "qec_pack_decisions_dev": (i, [vp, vp, vp, vp, sz, vp, vp]),
             "qec_monte_carlo": (i, [vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, f, i, i, sz,
                                     ctypes.POINTER(MCResult)]),
@@ -254,21 +270,48 @@ class DecoderGPU:
     """MI355X BP engine behind the reference's DecoderGPU slot (QEC_LDPC/DecoderGPU.h).
 
     engine: "auto" (wave-circulant kernel when the code has one, else sparse-graph),
-    "circulant" or "sparse" (include/qec_ldpc.h, QEC_ENGINE_*)."""
+    "circulant" or "sparse" (include/qec_ldpc.h, QEC_ENGINE_*).
+    max_batch: sizes the device-pointer workspace so the *_dev decodes allocate nothing for
+    batches up to it (graph capture); larger batches grow it on demand.
+    devices: a list of HIP device ordinals for a multi-device decoder (qec_decoder_create_multi):
+    the host-buffer calls, GetStatistics and monte_carlo shard their samples over the devices;
+    the *_dev calls go to one of parts()."""
 
-    def __init__(self, code, device=0, engine="auto"):
+    def __init__(self, code, device=0, engine="auto", max_batch=0, devices=None, _handle=None):
         self.code = code
-        h = lib().qec_decoder_create_engine(code.handle, int(device), 0, ENGINE[engine])
+        self._owned = _handle is None
+        if _handle is not None:
+            h = _handle
+        elif devices is not None:
+            devs = (ctypes.c_int * len(devices))(*[int(x) for x in devices])
+            h = lib().qec_decoder_create_multi(code.handle, devs, len(devices), int(max_batch))
+        else:
+            h = lib().qec_decoder_create_engine(code.handle, int(device), int(max_batch), ENGINE[engine])
         if not h:
             raise QecError(last_error())
         self._h = ctypes.c_void_p(h)
-        self.device = device
+        self.device = int(lib().qec_decoder_device(self._h))
+        self.num_parts = int(lib().qec_decoder_num_parts(self._h))
 
     def __del__(self):
         h = getattr(self, "_h", None)
-        if h and _lib is not None:
+        if h and _lib is not None and getattr(self, "_owned", False):
             _lib.qec_decoder_destroy(h)
-            self._h = None
+        self._h = None
+
+    def parts(self):
+        """Single-device views of a multi-device decoder's parts (or [self])."""
+        if self.num_parts == 1:
+            return [self]
+        out = []
+        for k in range(self.num_parts):
+            h = lib().qec_decoder_part(self._h, k)
+            if not h:
+                raise QecError(last_error())
+            p = DecoderGPU(self.code, _handle=h)
+            p._parent = self  # keeps the group (the owner of the part) alive
+            out.append(p)
+        return out
 
     def describe(self):
         buf = ctypes.create_string_buffer(256)
@@ -284,6 +327,11 @@ class DecoderGPU:
         _check(lib().qec_decoder_get_option(self._h, OPTION[name], ctypes.byref(v)), "qec_decoder_get_option")
         return v.value
 
+    def record_bytes(self):
+        """Bytes of one packed decision record: 2 ceil(n/8) + 1."""
+        return record_bytes(self.code.n)
+
+    # ---- host buffers ------------------------------------------------------------------
     def decode_batch(self, sX, sZ, p, max_iter, stop="ref", want_iters=False, want_q=False):
         """Host-buffer batch decode -> (eX, eZ, flags, iters|None, q|None)."""
         c = self.code
@@ -300,59 +348,154 @@ class DecoderGPU:
                                       _ptr(eX), _ptr(eZ), _ptr(flags), _ptr(iters), _ptr(q)), "qec_decode_batch")
         return eX, eZ, flags, iters, q
 
-    def decode_batch_dev(self, sX, sZ, p, max_iter, stop, eX, eZ, flags, iters=None, q=None, stream=None):
-        """Device-buffer batch decode on torch tensors (or raw int pointers), async on `stream`
-        (a torch.cuda.Stream, a raw hipStream_t int, or None = torch's current stream)."""
-        def addr(t):
-            if t is None:
-                return None
-            return t if isinstance(t, int) else t.data_ptr()
-        B = sX.shape[0] if hasattr(sX, "shape") else None
-        if B is None:
-            raise QecError("decode_batch_dev needs tensors with a shape")
-        if stream is None:
-            import torch
-            stream = torch.cuda.current_stream().cuda_stream
-        elif not isinstance(stream, int):
-            stream = stream.cuda_stream
-        _check(lib().qec_decode_batch_dev(self._h, addr(sX), addr(sZ), B, float(p), int(max_iter), STOP[stop],
-                                          addr(eX), addr(eZ), addr(flags), addr(iters), addr(q),
-                                          ctypes.c_void_p(stream)), "qec_decode_batch_dev")
+    def decode_batch_packed(self, sX, sZ, p, max_iter, stop="ref", want_iters=False):
+        """Host-buffer batch decode to packed decision records -> (records [B, record_bytes()], iters|None)."""
+        c = self.code
+        sX = np.atleast_2d(sX)
+        B = sX.shape[0]
+        sX = _u8(sX, (B, c.numEqsX))
+        sZ = _u8(sZ, (B, c.numEqsZ))
+        rec = np.empty((B, self.record_bytes()), dtype=np.uint8)
+        iters = np.empty((B, 2), dtype=np.int32) if want_iters else None
+        _check(lib().qec_decode_batch_packed(self._h, _ptr(sX), _ptr(sZ), B, float(p), int(max_iter), STOP[stop],
+                                             _ptr(rec), _ptr(iters)), "qec_decode_batch_packed")
+        return rec, iters
 
-    @staticmethod
-    def _stream(stream):
+    # ---- device buffers (torch tensors on this decoder's GPU) ---------------------------
+    def _stream(self, stream):
         if stream is None:
             import torch
-            return torch.cuda.current_stream().cuda_stream
+            return torch.cuda.current_stream(self.device).cuda_stream
         return stream if isinstance(stream, int) else stream.cuda_stream
+
+    def _t(self, t, name, dtype, shape, optional=False):
+        """Device pointer of tensor t after checking it is what the C ABI will read or write."""
+        if t is None:
+            if optional:
+                return None
+            raise QecError("%s: tensor required" % name)
+        import torch
+        if not isinstance(t, torch.Tensor):
+            raise QecError("%s: expected a torch tensor, got %s" % (name, type(t).__name__))
+        if not t.is_cuda or t.device.index != self.device:
+            raise QecError("%s: must be on cuda:%d (the decoder's device), is on %s" % (name, self.device, t.device))
+        if t.dtype != dtype:
+            raise QecError("%s: dtype must be %s, is %s" % (name, dtype, t.dtype))
+        if not t.is_contiguous():
+            raise QecError("%s: must be contiguous" % name)
+        if tuple(t.shape) != tuple(shape):
+            raise QecError("%s: shape must be %s, is %s" % (name, tuple(shape), tuple(t.shape)))
+        return t.data_ptr()
+
+    def _single(self, what):
+        if self.num_parts != 1:
+            raise QecError("%s: device buffers live on one GPU; call it on one of parts()" % what)
+
+    def decode_batch_dev(self, sX, sZ, p, max_iter, stop, eX, eZ, flags, iters=None, q=None, stream=None):
+        """Device-buffer batch decode on torch tensors, async on `stream` (a torch.cuda.Stream, a raw
+        hipStream_t int, or None = torch's current stream on the decoder's device)."""
+        import torch
+        self._single("decode_batch_dev")
+        c = self.code
+        B = sX.shape[0]
+        u8 = torch.uint8
+        args = (self._t(sX, "sX", u8, (B, c.numEqsX)), self._t(sZ, "sZ", u8, (B, c.numEqsZ)),
+                B, float(p), int(max_iter), STOP[stop],
+                self._t(eX, "eX", u8, (B, c.n)), self._t(eZ, "eZ", u8, (B, c.n)), self._t(flags, "flags", u8, (B,)),
+                self._t(iters, "iters", torch.int32, (B, 2), True),
+                self._t(q, "q", torch.float32, (B, (c.numEqsX + c.numEqsZ) * c.L), True))
+        _check(lib().qec_decode_batch_dev(self._h, *args, ctypes.c_void_p(self._stream(stream))), "qec_decode_batch_dev")
+
+    def decode_batch_packed_dev(self, sX, sZ, p, max_iter, stop, records, iters=None, q=None, stream=None):
+        """Device-buffer batch decode into packed decision records [B, record_bytes()] (uint8)."""
+        import torch
+        self._single("decode_batch_packed_dev")
+        c = self.code
+        B = sX.shape[0]
+        u8 = torch.uint8
+        args = (self._t(sX, "sX", u8, (B, c.numEqsX)), self._t(sZ, "sZ", u8, (B, c.numEqsZ)),
+                B, float(p), int(max_iter), STOP[stop],
+                self._t(records, "records", u8, (B, self.record_bytes())),
+                self._t(iters, "iters", torch.int32, (B, 2), True),
+                self._t(q, "q", torch.float32, (B, (c.numEqsX + c.numEqsZ) * c.L), True))
+        _check(lib().qec_decode_batch_packed_dev(self._h, *args, ctypes.c_void_p(self._stream(stream))),
+               "qec_decode_batch_packed_dev")
 
     def sample_depolarizing_dev(self, seed, start, p, x, z, stream=None):
         """Device Philox depolarising errors for samples [start, start + x.shape[0])."""
-        _check(lib().qec_sample_depolarizing_dev(self._h, seed & (2 ** 64 - 1), start, x.shape[0], float(p),
-                                                 x.data_ptr(), z.data_ptr(), ctypes.c_void_p(self._stream(stream))),
+        import torch
+        self._single("sample_depolarizing_dev")
+        B, n = x.shape[0], self.code.n
+        _check(lib().qec_sample_depolarizing_dev(self._h, seed & (2 ** 64 - 1), start, B, float(p),
+                                                 self._t(x, "x", torch.uint8, (B, n)),
+                                                 self._t(z, "z", torch.uint8, (B, n)),
+                                                 ctypes.c_void_p(self._stream(stream))),
                "qec_sample_depolarizing_dev")
 
+    def sample_syndrome_dev(self, seed, start, p, sX, sZ, errp=None, stream=None):
+        """Fused front end: syndromes of the depolarising errors of samples [start, start + B)
+        (the sample_depolarizing_dev stream), optionally the errors bit-packed (errp [B, 2 ceil(n/8)])."""
+        import torch
+        self._single("sample_syndrome_dev")
+        c = self.code
+        B = sX.shape[0]
+        _check(lib().qec_sample_syndrome_dev(self._h, seed & (2 ** 64 - 1), start, B, float(p),
+                                             self._t(sX, "sX", torch.uint8, (B, c.numEqsX)),
+                                             self._t(sZ, "sZ", torch.uint8, (B, c.numEqsZ)),
+                                             self._t(errp, "errp", torch.uint8, (B, 2 * ((c.n + 7) // 8)), True),
+                                             ctypes.c_void_p(self._stream(stream))), "qec_sample_syndrome_dev")
+
     def syndrome_dev(self, x, z, sX, sZ, stream=None):
-        _check(lib().qec_syndrome_dev(self._h, x.data_ptr(), z.data_ptr(), x.shape[0], sX.data_ptr(), sZ.data_ptr(),
+        import torch
+        self._single("syndrome_dev")
+        c = self.code
+        B = x.shape[0]
+        u8 = torch.uint8
+        _check(lib().qec_syndrome_dev(self._h, self._t(x, "x", u8, (B, c.n)), self._t(z, "z", u8, (B, c.n)), B,
+                                      self._t(sX, "sX", u8, (B, c.numEqsX)), self._t(sZ, "sZ", u8, (B, c.numEqsZ)),
                                       ctypes.c_void_p(self._stream(stream))), "qec_syndrome_dev")
 
     def statistics_dev(self, x, z, eX, eZ, flags, counters, stream=None):
         """Adds the batch's CodeStatistics counters into the int64 device tensor counters[8]
         (order: MC_COUNTERS)."""
-        _check(lib().qec_statistics_dev(self._h, x.data_ptr(), z.data_ptr(), eX.data_ptr(), eZ.data_ptr(),
-                                        flags.data_ptr(), x.shape[0], counters.data_ptr(),
+        import torch
+        self._single("statistics_dev")
+        c = self.code
+        B = x.shape[0]
+        u8 = torch.uint8
+        _check(lib().qec_statistics_dev(self._h, self._t(x, "x", u8, (B, c.n)), self._t(z, "z", u8, (B, c.n)),
+                                        self._t(eX, "eX", u8, (B, c.n)), self._t(eZ, "eZ", u8, (B, c.n)),
+                                        self._t(flags, "flags", u8, (B,)), B,
+                                        self._t(counters, "counters", torch.int64, (len(MC_COUNTERS),)),
                                         ctypes.c_void_p(self._stream(stream))), "qec_statistics_dev")
 
-    def record_bytes(self):
-        """Bytes of one decision record (qec_pack_decisions_dev): 2 ceil(n/8) + 1."""
-        return 2 * ((self.code.n + 7) // 8) + 1
+    def statistics_packed_dev(self, errp, records, counters, iters=None, stream=None):
+        """Adds the counters of packed errors + packed decision records into counters (int64 device
+        tensor: [8] = MC_COUNTERS, or [10] = MC_COUNTERS_ALL when iters [B, 2] is given)."""
+        import torch
+        self._single("statistics_packed_dev")
+        c = self.code
+        B = errp.shape[0]
+        nc = len(MC_COUNTERS_ALL) if iters is not None else len(MC_COUNTERS)
+        _check(lib().qec_statistics_packed_dev(self._h, self._t(errp, "errp", torch.uint8, (B, 2 * ((c.n + 7) // 8))),
+                                               self._t(records, "records", torch.uint8, (B, self.record_bytes())),
+                                               self._t(iters, "iters", torch.int32, (B, 2), True), B,
+                                               self._t(counters, "counters", torch.int64, (nc,)),
+                                               ctypes.c_void_p(self._stream(stream))), "qec_statistics_packed_dev")
 
     def pack_decisions_dev(self, eX, eZ, flags, out, stream=None):
         """Bit-packs a decoded device batch into out [B, record_bytes()] (uint8 device tensor)."""
-        _check(lib().qec_pack_decisions_dev(self._h, eX.data_ptr(), eZ.data_ptr(), flags.data_ptr(), eX.shape[0],
-                                            out.data_ptr(), ctypes.c_void_p(self._stream(stream))),
-               "qec_pack_decisions_dev")
+        import torch
+        self._single("pack_decisions_dev")
+        c = self.code
+        B = eX.shape[0]
+        u8 = torch.uint8
+        _check(lib().qec_pack_decisions_dev(self._h, self._t(eX, "eX", u8, (B, c.n)), self._t(eZ, "eZ", u8, (B, c.n)),
+                                            self._t(flags, "flags", u8, (B,)), B,
+                                            self._t(out, "out", u8, (B, self.record_bytes())),
+                                            ctypes.c_void_p(self._stream(stream))), "qec_pack_decisions_dev")
 
+    # ---- Monte-Carlo ---------------------------------------------------------------------
     def monte_carlo(self, seed, start, count, p, max_iter, stop="syndrome", batch=65536):
         """Device Monte-Carlo run (sample -> syndrome -> decode -> statistics); returns a dict."""
         r = MCResult()

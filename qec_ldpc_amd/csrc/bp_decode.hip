@@ -34,6 +34,7 @@
 #include <cstdint>
 #include <cstdio>
 
+#include "qec_device.h"
 #include "qec_internal.h"
 
 #pragma clang fp contract(off)
@@ -153,8 +154,15 @@ struct BpArgs {
     int32_t* iters;
     float* q;
     const int32_t* perm;  // dispatch order (schedule.hip): group slot k decodes syndrome perm[k]; null = batch order
+    // packed decision records (qec_decode_batch_packed_dev): per syndrome eX bits, eZ bits (nb bytes
+    // each, bit j of byte k = qubit 8k + j), then the flags byte; null = byte outputs eX / eZ / flags
+    uint8_t* rec;
+    // sector-split launches: one word per syndrome, zeroed before the launch; each sector ORs in its
+    // flags plus a done bit and the second one writes the merged flags byte (plain store)
+    uint32_t* merge;
     long long B;
     int P, G, n, mX, mZ;
+    int nb, recBytes;  // ceil(n / 8), 2 nb + 1
     float errorProbability;
     int maxIter, stop;
     int hardPaths;  // QEC_HP_* bits: hard-message paths / cycle jump (QEC_OPT_HARD_PATHS, QEC_OPT_CYCLE_JUMP)
@@ -842,10 +850,57 @@ __device__ __forceinline__ uint32_t load_sbits(const BpArgs& a, const Lane& ln, 
     return sbits;
 }
 
+// ---- decision output ---------------------------------------------------------------
+// LDS staging of one wave's decisions for the packed records: G groups of npad = 8 nb bytes
+// (a syndrome's n decision bytes, zero-padded to whole 8-byte words).
+template <int L, class SH>
+constexpr int stage_bytes_per_wave()
+{
+    if constexpr (SH::kStatic) {
+        constexpr int n = L * SH::kP;
+        return (64 / SH::kP) * ((n + 7) / 8) * 8;
+    } else {
+        return 64 * (L + 8);  // G (L P + 7) <= 64 L + 7 G for any P <= 64
+    }
+}
+
+// Hard decisions of this lane's L variables (bit l of hdmask: variable (l, (i + C[l]) mod P)) to
+// eX / eZ bytes, or, for a packed launch, through the wave's LDS stage into the record's nb bytes of
+// this sector: lane i of a group packs bytes i, i + P, ... (8 staged bytes each, one 8-byte LDS read).
+template <int L, int SEC, class SH>
+__device__ __forceinline__ void emit_decisions(const BpArgs& a, const Lane& ln, long long b, bool in_range,
+                                               uint32_t hdmask, uint8_t* __restrict__ stage)
+{
+    const int P = SH::P(a);
+    const int i = ln.i;
+    if (a.rec == nullptr) {
+        uint8_t* __restrict__ e = SEC ? a.eZ : a.eX;
+        if (in_range) {
+#pragma unroll
+            for (int l = 0; l < L; ++l)
+                e[b * (long long)a.n + l * P + wrap(i + SH::template coloff<SEC>(a, l), P)] = (uint8_t)((hdmask >> l) & 1u);
+        }
+        return;
+    }
+    const int nb = a.nb;
+    uint8_t* __restrict__ sg = stage + (ln.gb / P) * (nb * 8);
+    if (in_range) {
+#pragma unroll
+        for (int l = 0; l < L; ++l) sg[l * P + wrap(i + SH::template coloff<SEC>(a, l), P)] = (uint8_t)((hdmask >> l) & 1u);
+        for (int k = a.n + i; k < nb * 8; k += P) sg[k] = 0;
+    }
+    wave_sync();
+    if (in_range) {
+        uint8_t* __restrict__ out = a.rec + b * (long long)a.recBytes + SEC * nb;
+        for (int k = i; k < nb; k += P) out[k] = (uint8_t)pack8(*reinterpret_cast<const uint64_t*>(sg + 8 * k));
+    }
+    wave_sync();  // the next sector reuses the stage
+}
+
 template <int R, int L, int SEC, int STOP, class SH, class TU>
 __device__ __forceinline__ void decode_sector(const BpArgs& a, Lane& ln, long long b, bool in_range, float pp,
                                               uint32_t sbits, const float* __restrict__ tab0, uint32_t& flags,
-                                              int& iters_out)
+                                              int& iters_out, uint8_t* __restrict__ stage)
 {
     const int i = ln.i, gb = ln.gb;
     const int P = SH::P(a);
@@ -919,9 +974,9 @@ __device__ __forceinline__ void decode_sector(const BpArgs& a, Lane& ln, long lo
         return;
     }
     // ---- post-processing of Decode (DecoderCPU.h:354-384) ----
-    uint8_t* __restrict__ e = SEC ? a.eZ : a.eX;
     const int* et = SH::template table<SEC>(a);
     bool conv, syn_ok;
+    uint32_t hdmask = 0;  // e[v] of this lane's variables (l, (i + C[l]) mod P), bit l
     if (TU::kSaturate && all_live(st_agreed, in_range)) {
         // Every live group's state is hard and each variable's R messages are equal: the hard
         // decision is the value on any one of its edges (row 0's, rotation S[0][l], 0 with the
@@ -929,10 +984,8 @@ __device__ __forceinline__ void decode_sector(const BpArgs& a, Lane& ln, long lo
         // own L messages (each equals its variable's decision), and every message is outside
         // (0.01, 0.99).  Same outputs as the general path below, without its 2 R L rotations.
 #pragma unroll
-        for (int l = 0; l < L; ++l) {
-            const bool hd = rot<SH>(msg[0][l], ln, SH::template shift<SEC, L>(et, 0, l)) >= 0.5f;
-            if (in_range) e[b * (long long)a.n + l * P + wrap(i + SH::template coloff<SEC>(a, l), P)] = (uint8_t)hd;
-        }
+        for (int l = 0; l < L; ++l)
+            hdmask |= (uint32_t)(rot<SH>(msg[0][l], ln, SH::template shift<SEC, L>(et, 0, l)) >= 0.5f) << l;
         bool match = true;
 #pragma unroll
         for (int r = 0; r < R; ++r) {
@@ -945,7 +998,6 @@ __device__ __forceinline__ void decode_sector(const BpArgs& a, Lane& ln, long lo
         syn_ok = group_all(match, gb, P);
     } else {
         conv = group_all(lane_converged<R, L>(msg), gb, P);
-        uint32_t hdmask = 0;
 #pragma unroll
         for (int l = 0; l < L; ++l) {
             bool hd = false;  // e[v] = any edge message >= 0.5f (DecoderCPU.h:354-373)
@@ -955,10 +1007,10 @@ __device__ __forceinline__ void decode_sector(const BpArgs& a, Lane& ln, long lo
                 hd |= rot<SH>(msg[r][l], ln, sh) >= 0.5f;
             }
             hdmask |= (uint32_t)hd << l;
-            if (in_range) e[b * (long long)a.n + l * P + wrap(i + SH::template coloff<SEC>(a, l), P)] = (uint8_t)hd;
         }
         syn_ok = group_all(lane_syndrome_ok<R, L, SEC, SH>(a, hdmask, sbits, ln), gb, P);
     }
+    emit_decisions<L, SEC, SH>(a, ln, b, in_range, hdmask, stage);
 
     if (!syn_ok) flags |= SEC ? QEC_SYNDROME_FAIL_Z : QEC_SYNDROME_FAIL_X;
     if (!conv) flags |= SEC ? QEC_CONVERGENCE_FAIL_Z : QEC_CONVERGENCE_FAIL_X;
@@ -1015,6 +1067,10 @@ void bp_decode_kernel(const BpArgs a)
             tab0[e] = e < kTabX ? table0_entry<RX, L>(ppt, e) : table0_entry<RZ, L>(ppt, e - kTabX);
         __syncthreads();
     }
+    // this wave's decision stage for packed records (emit_decisions)
+    constexpr int kStage = stage_bytes_per_wave<L, SH>();
+    __shared__ __attribute__((aligned(8))) uint8_t stage_all[waves_per_block<TU>() * kStage];
+    uint8_t* stage = stage_all + (threadIdx.x >> 6) * kStage;
     const long long grp = SPLIT ? wave >> 1 : wave;
     const long long slot = grp * G + g;
     const bool in_range = (g < G) && (slot < a.B);
@@ -1033,17 +1089,20 @@ void bp_decode_kernel(const BpArgs a)
     // both sectors' syndrome loads are issued up front: the Z load's latency hides behind X
     const uint32_t sbX = doX ? load_sbits<RX, 0, SH>(a, ln, b, in_range) : 0u;
     uint32_t sbZ = (QEC_PREFETCH_Z && (!doX || !SPLIT)) ? load_sbits<RZ, 1, SH>(a, ln, b, in_range) : 0u;
-    if (doX) decode_sector<RX, L, 0, STOP, SH, TU>(a, ln, b, in_range, pp, sbX, tab0, flags, itX);
+    if (doX) decode_sector<RX, L, 0, STOP, SH, TU>(a, ln, b, in_range, pp, sbX, tab0, flags, itX, stage);
     if (!QEC_PREFETCH_Z && (!doX || !SPLIT)) sbZ = load_sbits<RZ, 1, SH>(a, ln, b, in_range);
-    if (!doX || !SPLIT) decode_sector<RZ, L, 1, STOP, SH, TU>(a, ln, b, in_range, pp, sbZ, tab0 + kTabX, flags, itZ);
+    if (!doX || !SPLIT)
+        decode_sector<RZ, L, 1, STOP, SH, TU>(a, ln, b, in_range, pp, sbZ, tab0 + kTabX, flags, itZ, stage);
     if (in_range && i == 0) {
+        uint8_t* fdst = a.rec != nullptr ? a.rec + b * (long long)a.recBytes + 2 * a.nb : a.flags + b;
         if constexpr (!SPLIT) {
-            a.flags[b] = (uint8_t)flags;
-        } else if (flags != 0) {
-            // OR this sector's bits into the byte through its aligned 32-bit word (the other
-            // three bytes of the word get | 0)
-            const uintptr_t addr = reinterpret_cast<uintptr_t>(a.flags + b);
-            atomicOr(reinterpret_cast<unsigned int*>(addr & ~(uintptr_t)3), flags << (8 * (addr & 3)));
+            *fdst = (uint8_t)flags;
+        } else {
+            // the two sectors meet in the syndrome's merge word: whichever finds the other's done
+            // bit already set writes the merged byte
+            const uint32_t mine = doX ? 0x100u : 0x200u;
+            const uint32_t old = atomicOr(&a.merge[b], flags | mine);
+            if (old & (0x300u ^ mine)) *fdst = (uint8_t)((old | flags) & 0xFFu);
         }
         if (a.iters != nullptr) {
             if (doX) a.iters[2 * b] = itX;
@@ -1074,7 +1133,9 @@ using ShiftsP7 = GeneratedShifts<3, 3, 6, 7, 2, 3, TuneP7::kRelabel, TuneP7::kMa
 KernelFn p61_minreg_kernel(int stop, bool split);  // bp_decode_p61.hip
 KernelFn p7_minreg_kernel(int stop, bool split);   // bp_decode_p61.hip
 
-#ifdef QEC_P61_MINREG_TU
+KernelFn phase_kernel(int P, int stop);  // bp_decode_phase.hip
+
+#if defined(QEC_P61_MINREG_TU)
 KernelFn p61_minreg_kernel(int stop, bool split)
 {
     if (stop == QEC_STOP_REF)
@@ -1092,6 +1153,22 @@ KernelFn p7_minreg_kernel(int stop, bool split)
                      : bp_decode_kernel<3, 3, 6, QEC_STOP_SYNDROME, ShiftsP7, TuneP7MinReg, false>;
     return nullptr;
 }
+#elif defined(QEC_PHASE_TU)
+// The instrumented kernels of the shipped codes (QEC_OPT_PHASE_STATS, one wave per syndrome):
+// iters[] reports per sector soft | hard << 8 | agreed << 16 | jumped << 24 iterations.
+struct TuneP61Phase : TuneP61 {};
+struct TuneP7Phase : TuneP7 {};
+KernelFn phase_kernel(int P, int stop)
+{
+    if (P == 61) {
+        if (stop == QEC_STOP_REF) return bp_decode_kernel<4, 5, 10, QEC_STOP_REF, ShiftsP61, TuneP61Phase, false>;
+        if (stop == QEC_STOP_FIXED) return bp_decode_kernel<4, 5, 10, QEC_STOP_FIXED, ShiftsP61, TuneP61Phase, false>;
+        return bp_decode_kernel<4, 5, 10, QEC_STOP_SYNDROME, ShiftsP61, TuneP61Phase, false>;
+    }
+    if (stop == QEC_STOP_REF) return bp_decode_kernel<3, 3, 6, QEC_STOP_REF, ShiftsP7, TuneP7Phase, false>;
+    if (stop == QEC_STOP_FIXED) return bp_decode_kernel<3, 3, 6, QEC_STOP_FIXED, ShiftsP7, TuneP7Phase, false>;
+    return bp_decode_kernel<3, 3, 6, QEC_STOP_SYNDROME, ShiftsP7, TuneP7Phase, false>;
+}
 #else
 
 struct Variant {
@@ -1102,6 +1179,7 @@ struct Variant {
     int waves_per_block;
     KernelFn fn[3];     // indexed by stop rule
     KernelFn split[3];  // the same with one wave per sector (nullptr: not instantiated)
+    KernelFn phase[3];  // QEC_OPT_PHASE_STATS: instrumented kernels (shipped codes only)
     const char* name;
 };
 
@@ -1112,6 +1190,7 @@ static Variant make_variant(int P, int S, int T, const char* name)
               {bp_decode_kernel<J, K, L, QEC_STOP_REF, SH, TU, false>,
                bp_decode_kernel<J, K, L, QEC_STOP_FIXED, SH, TU, false>,
                bp_decode_kernel<J, K, L, QEC_STOP_SYNDROME, SH, TU, false>},
+              {nullptr, nullptr, nullptr},
               {nullptr, nullptr, nullptr},
               name};
     if constexpr (WITH_SPLIT) {
@@ -1150,6 +1229,7 @@ static Variant gen()
 static Variant gen_p61()
 {
     Variant v = gen<4, 5, 10, 61, 9, 49, TuneP61>();
+    for (int stop : {QEC_STOP_REF, QEC_STOP_FIXED, QEC_STOP_SYNDROME}) v.phase[stop] = phase_kernel(61, stop);
     if (QEC_P61_MINREG) {
         for (int stop : {QEC_STOP_REF, QEC_STOP_FIXED}) {
             v.fn[stop] = p61_minreg_kernel(stop, false);
@@ -1162,6 +1242,7 @@ static Variant gen_p61()
 static Variant gen_p7()
 {
     Variant v = gen<3, 3, 6, 7, 2, 3, TuneP7>();
+    for (int stop : {QEC_STOP_REF, QEC_STOP_FIXED, QEC_STOP_SYNDROME}) v.phase[stop] = phase_kernel(7, stop);
     if (QEC_P61_MINREG) {
         v.fn[QEC_STOP_SYNDROME] = p7_minreg_kernel(QEC_STOP_SYNDROME, false);
         v.split[QEC_STOP_SYNDROME] = p7_minreg_kernel(QEC_STOP_SYNDROME, true);
@@ -1218,39 +1299,54 @@ bool decode_uses_split(const void* variant, int stop, int split)
     return (split == 2 || (split == 1 && v->split_auto)) && v->split[stop] != nullptr;
 }
 
+bool decode_has_phase_stats(const void* variant, int stop)
+{
+    return static_cast<const Variant*>(variant)->phase[stop] != nullptr;
+}
+
 int launch_decode(const void* variant, const Code& c, const uint8_t* sX, const uint8_t* sZ, long long B,
                   float errorProbability, int maxIter, int stop, uint8_t* eX, uint8_t* eZ, uint8_t* flags,
-                  int32_t* iters, float* q, int hardPaths, const int32_t* perm, int split, bool flags_zeroed,
-                  hipStream_t stream)
+                  uint8_t* rec, int32_t* iters, float* q, int hardPaths, const int32_t* perm, int split,
+                  uint32_t* merge, bool merge_zeroed, hipStream_t stream)
 {
     const Variant* v = static_cast<const Variant*>(variant);
     if (B <= 0) return QEC_OK;
     BpArgs a{};
     a.sX = sX; a.sZ = sZ; a.eX = eX; a.eZ = eZ; a.flags = flags; a.iters = iters; a.q = q;
+    a.rec = rec;
     a.perm = perm;
-    split = decode_uses_split(variant, stop, split);
-    if (split && !flags_zeroed && hipMemsetAsync(flags, 0, (size_t)B, stream) != hipSuccess)
-        return fail(QEC_ERR_HIP, "bp_decode: flags memset failed");
+    const bool phase = (hardPaths & QEC_HP_PHASE) != 0;
+    if (phase && v->phase[stop] == nullptr)
+        return fail(QEC_ERR_UNSUPPORTED, "bp_decode: no phase-statistics kernel for this code");
+    split = !phase && decode_uses_split(variant, stop, split) && merge != nullptr;
+    if (split) {
+        a.merge = merge;
+        if (!merge_zeroed && hipMemsetAsync(merge, 0, (size_t)B * sizeof(uint32_t), stream) != hipSuccess)
+            return fail(QEC_ERR_HIP, "bp_decode: merge-word memset failed");
+    }
     a.B = B;
     a.P = c.P;
     a.G = 64 / c.P;
     a.n = c.n; a.mX = c.mX; a.mZ = c.mZ;
+    a.nb = (c.n + 7) / 8;
+    a.recBytes = 2 * a.nb + 1;
     a.errorProbability = errorProbability;
     a.maxIter = maxIter < 0 ? 0 : maxIter;
     a.stop = stop;
-    a.hardPaths = hardPaths;
+    a.hardPaths = hardPaths & (QEC_HP_FORMS | QEC_HP_CYCLE);
     relabel(c.EX.data(), c.J, c.L, c.P, v->relabel, a.SX, a.DX, a.CX);
     relabel(c.EZ.data(), c.K, c.L, c.P, v->relabel, a.SZ, a.DZ, a.CZ);
     const int wavesPerBlock = v->waves_per_block;
     const long long waves = (B + a.G - 1) / a.G * (split ? 2 : 1);
     const long long blocks = (waves + wavesPerBlock - 1) / wavesPerBlock;
     if (blocks > 0x7fffffffLL) return fail(QEC_ERR_ARG, "batch too large for one launch");
-    hipLaunchKernelGGL(split ? v->split[stop] : v->fn[stop], dim3((unsigned)blocks), dim3(64 * wavesPerBlock), 0, stream, a);
+    hipLaunchKernelGGL(phase ? v->phase[stop] : split ? v->split[stop] : v->fn[stop], dim3((unsigned)blocks),
+                       dim3(64 * wavesPerBlock), 0, stream, a);
     hipError_t err = hipGetLastError();
     if (err != hipSuccess) return fail(QEC_ERR_HIP, std::string("bp_decode launch: ") + hipGetErrorString(err));
     return QEC_OK;
 }
 
-#endif  // QEC_P61_MINREG_TU
+#endif  // QEC_P61_MINREG_TU / QEC_PHASE_TU
 
 }  // namespace qec

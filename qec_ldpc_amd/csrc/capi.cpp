@@ -7,6 +7,7 @@
 #include <new>
 #include <stdexcept>
 #include <algorithm>
+#include <thread>
 
 #include "../../include/HostDeviceArray.h"
 #include "qec_internal.h"
@@ -16,19 +17,19 @@ const char* last_error_cstr();
 const void* select_variant(const Code& c, std::string& name);
 int launch_decode(const void* variant, const Code& c, const uint8_t* sX, const uint8_t* sZ, long long B,
                   float errorProbability, int maxIter, int stop, uint8_t* eX, uint8_t* eZ, uint8_t* flags,
-                  int32_t* iters, float* q, int hardPaths, const int32_t* perm, int split, bool flags_zeroed,
-                  hipStream_t stream);
+                  uint8_t* rec, int32_t* iters, float* q, int hardPaths, const int32_t* perm, int split,
+                  uint32_t* merge, bool merge_zeroed, hipStream_t stream);
 size_t schedule_workspace_bytes(long long B, int mX, int mZ);
 long long schedule_max_batch();
 int launch_schedule(const uint8_t* sX, const uint8_t* sZ, long long B, int mX, int mZ, void* ws,
-                    uint8_t* zero_flags, int32_t** perm_out, hipStream_t st);
+                    uint32_t* zero_merge, int32_t** perm_out, hipStream_t st);
 bool decode_uses_split(const void* variant, int stop, int split);
+bool decode_has_phase_stats(const void* variant, int stop);
 int launch_sample_depolarizing(uint64_t seed, uint64_t start, long long B, int n, float p, uint8_t* x, uint8_t* z,
                                hipStream_t st);
-int launch_errors_from_draws(const int32_t* idx, const uint8_t* type, long long B, int W, int n, uint8_t* x,
-                             uint8_t* z, hipStream_t st);
-int launch_syndrome(const Code& c, const int32_t* chkVar, const uint8_t* x, const uint8_t* z, long long B,
-                    uint8_t* sX, uint8_t* sZ, hipStream_t st);
+int launch_mc_errors_syndrome(int src, const McArgsHost& h, hipStream_t st);
+int launch_statistics_packed(const Code& c, const uint64_t* imp_rec_dev, const uint8_t* errp, const uint8_t* rec,
+                             const int32_t* iters, long long B, unsigned long long* counters, hipStream_t st);
 void* sparse_plan_create(const Code& c, int device);
 void sparse_plan_free(void* plan);
 const char* sparse_plan_name(const void* plan);
@@ -48,6 +49,9 @@ struct qec_code {
     Code c;
 };
 
+
+// One decoder handle: a device engine (wave-circulant variant or sparse-graph plan) plus the
+// workspaces its entry points share, or a multi-device group of such handles (parts).
 struct qec_decoder {
     std::shared_ptr<const Code> code;
     int device = 0;
@@ -59,18 +63,39 @@ struct qec_decoder {
     int cycle_jump = 1;             // QEC_OPT_CYCLE_JUMP
     int schedule = 1;               // QEC_OPT_SCHEDULE (0 off, 1 auto, 2 always)
     int sector_split = 1;           // QEC_OPT_SECTOR_SPLIT (0 off, 1 auto, 2 on)
-    DeviceArray<uint8_t> sched;     // dispatch-order workspace (schedule.hip)
-    hipStream_t stream = nullptr;
-    // staging for the host-pointer entry point (DecoderGPU's device vectors, DecoderGPU.h:28-35)
-    DeviceArray<uint8_t> sX, sZ, eX, eZ, flags;
+    int phase_stats = 0;            // QEC_OPT_PHASE_STATS
+    // workspace shared by every launch of this handle (dispatch order, split-flag merge words,
+    // sparse byte staging for packed output); ws_ev marks the last launch that used it, so a call
+    // on another stream waits for it (stream-ordered reuse)
+    DeviceArray<uint8_t> sched;
+    DeviceArray<uint32_t> merge;
+    hipEvent_t ws_ev = nullptr;
+    hipStream_t ws_stream = nullptr;
+    bool ws_used = false;
+    hipStream_t stream = nullptr;   // the host-pointer and Monte-Carlo entry points' stream
+    // staging for the host-pointer entry points (DecoderGPU's device vectors, DecoderGPU.h:28-35)
+    DeviceArray<uint8_t> sX, sZ, eX, eZ, flags, rec;
     DeviceArray<int32_t> iters;
     DeviceArray<float> q;
     // Monte-Carlo workspace (qec_monte_carlo / qec_get_statistics)
-    DeviceArray<uint64_t> imp;  // bit-packed non-zero I-P rows
-    DeviceArray<uint8_t> mx, mz, msX, msZ, meX, meZ, mfl, mtype;
+    DeviceArray<uint64_t> imp;      // bit-packed non-zero I-P rows, qubit layout (statistics_kernel)
+    DeviceArray<uint64_t> imp_rec;  // the same rows in the decision-record layout (statistics_packed_kernel)
+    DeviceArray<uint8_t> msX, msZ, merrp, mrec, mtype;
     DeviceArray<int32_t> mit, midx;
     DeviceArray<unsigned long long> mcount;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    // multi-device group (qec_decoder_create_multi): the parts do the work, this handle only routes
+    std::vector<qec_decoder*> parts;
+
+    ~qec_decoder()
+    {
+        for (qec_decoder* p : parts) delete p;
+        if (parts.empty()) {
+            (void)hipSetDevice(device);
+            if (ws_ev) (void)hipEventDestroy(ws_ev);
+            if (stream) (void)hipStreamDestroy(stream);
+            if (sparse) sparse_plan_free(sparse);
+        }
+    }
 };
 
 #define QEC_HIP_CHECK(expr)                                                                     \
@@ -78,6 +103,79 @@ struct qec_decoder {
         hipError_t e_ = (expr);                                                                  \
         if (e_ != hipSuccess) return fail(QEC_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
     } while (0)
+
+namespace {
+
+// Makes `device` current for the scope of an entry point and restores the caller's device.
+struct DeviceGuard {
+    int prev = -1;
+    hipError_t err;
+    explicit DeviceGuard(int device)
+    {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        err = hipSetDevice(device);
+    }
+    ~DeviceGuard()
+    {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
+#define QEC_DEVICE_SCOPE(dev)                                                                      \
+    DeviceGuard guard_(dev);                                                                       \
+    if (guard_.err != hipSuccess) return fail(QEC_ERR_HIP, std::string("hipSetDevice: ") + hipGetErrorString(guard_.err))
+
+bool capturing(hipStream_t st)
+{
+    hipStreamCaptureStatus s = hipStreamCaptureStatusNone;
+    return hipStreamIsCapturing(st, &s) == hipSuccess && s != hipStreamCaptureStatusNone;
+}
+
+// Grow a workspace buffer to n elements.  Refused while `st` is being captured into a graph (an
+// allocation there would be invalid): size the decoder with max_batch instead.
+template <class T>
+int ws_reserve(DeviceArray<T>& a, size_t n, hipStream_t st, const char* what)
+{
+    if (n <= a.capacity()) return QEC_OK;
+    if (capturing(st))
+        return fail(QEC_ERR_ARG, std::string(what) + ": the workspace is smaller than this batch and the stream is "
+                                                     "being captured; create the decoder with max_batch >= B");
+    try {
+        a.reserve(n);
+    } catch (const std::exception& ex) {
+        return fail(QEC_ERR_NOMEM, std::string(what) + ": " + ex.what());
+    }
+    return QEC_OK;
+}
+
+// Stream-ordered use of the handle's workspace: a launch on a stream other than the previous
+// one first waits for the previous launch's completion event.  Launches captured into a graph
+// neither wait nor record (an event outside the capture cannot be waited on inside it): the
+// graph's replays are ordered by its launcher.
+int ws_acquire(qec_decoder* d, hipStream_t st)
+{
+    if (d->ws_used && st != d->ws_stream && !capturing(st)) QEC_HIP_CHECK(hipStreamWaitEvent(st, d->ws_ev, 0));
+    return QEC_OK;
+}
+int ws_release(qec_decoder* d, hipStream_t st)
+{
+    if (capturing(st)) return QEC_OK;
+    QEC_HIP_CHECK(hipEventRecord(d->ws_ev, st));
+    d->ws_used = true;
+    d->ws_stream = st;
+    return QEC_OK;
+}
+
+std::vector<qec_decoder*> parts_of(qec_decoder* d)
+{
+    if (d->parts.empty()) return {d};
+    return d->parts;
+}
+
+// contiguous shard k of n over [0, B): [k B / n, (k + 1) B / n)
+long long shard_lo(long long B, int k, int n) { return (long long)((__int128)B * k / n); }
+
+}  // namespace
 
 extern "C" {
 
@@ -158,6 +256,7 @@ int qec_code_check_logical(const qec_code* h, const uint8_t* ex, const uint8_t* 
     return QEC_OK;
 }
 
+
 qec_decoder* qec_decoder_create(const qec_code* h, int device, size_t max_batch)
 {
     return qec_decoder_create_engine(h, device, max_batch, QEC_ENGINE_AUTO);
@@ -184,8 +283,9 @@ qec_decoder* qec_decoder_create_engine(const qec_code* h, int device, size_t max
         return nullptr;
     }
     if (device >= ndev) { fail(QEC_ERR_ARG, "qec_decoder_create: device ordinal out of range"); return nullptr; }
-    if (hipSetDevice(device) != hipSuccess) { fail(QEC_ERR_HIP, "hipSetDevice failed"); return nullptr; }
-    auto* d = new (std::nothrow) qec_decoder;
+    DeviceGuard guard(device);
+    if (guard.err != hipSuccess) { fail(QEC_ERR_HIP, "hipSetDevice failed"); return nullptr; }
+    std::unique_ptr<qec_decoder> d(new (std::nothrow) qec_decoder);
     if (!d) { fail(QEC_ERR_NOMEM, "qec_decoder_create: out of memory"); return nullptr; }
     d->code = std::make_shared<const Code>(h->c);
     d->device = device;
@@ -194,49 +294,86 @@ qec_decoder* qec_decoder_create_engine(const qec_code* h, int device, size_t max
     if (!v) {  // AUTO without a wave-circulant kernel, or SPARSE requested
         d->engine = QEC_ENGINE_SPARSE;
         d->sparse = sparse_plan_create(*d->code, device);
-        if (!d->sparse) { delete d; return nullptr; }  // error text set by the plan
+        if (!d->sparse) return nullptr;  // error text set by the plan
         d->variant_name = sparse_plan_name(d->sparse);
     }
-    if (hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking) != hipSuccess) {
-        delete d;
-        fail(QEC_ERR_HIP, "hipStreamCreate failed");
+    if (hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&d->ws_ev, hipEventDisableTiming) != hipSuccess) {
+        fail(QEC_ERR_HIP, "qec_decoder_create: stream / event creation failed");
         return nullptr;
     }
     try {
-        // the dispatch-order workspace is sized up front so that qec_decode_batch_dev allocates
+        // the device-pointer workspace is sized up front so that the _dev entry points allocate
         // nothing for batches up to max_batch (graph capture); staging grows on demand
-        if (max_batch > 0 && d->variant && (long long)max_batch <= schedule_max_batch())
-            d->sched.reserve(schedule_workspace_bytes((long long)max_batch, d->code->mX, d->code->mZ));
+        if (max_batch > 0 && d->variant) {
+            if ((long long)max_batch <= schedule_max_batch())
+                d->sched.reserve(schedule_workspace_bytes((long long)max_batch, d->code->mX, d->code->mZ));
+            d->merge.reserve(max_batch);
+        }
+        if (max_batch > 0 && d->sparse) {
+            d->eX.reserve(max_batch * d->code->n);
+            d->eZ.reserve(max_batch * d->code->n);
+            d->flags.reserve(max_batch);
+        }
         if (!d->code->imp_rows.empty()) {
             d->imp.reserve(d->code->imp_rows.size());
-            if (hipMemcpy(d->imp.data(), d->code->imp_rows.data(), d->code->imp_rows.size() * sizeof(uint64_t),
-                          hipMemcpyHostToDevice) != hipSuccess)
-                throw std::runtime_error("I-P upload");
+            hip_throw(hipMemcpy(d->imp.data(), d->code->imp_rows.data(), d->code->imp_rows.size() * sizeof(uint64_t),
+                                hipMemcpyHostToDevice), "I-P upload");
+            d->imp_rec.reserve(d->code->imp_rows_rec.size());
+            hip_throw(hipMemcpy(d->imp_rec.data(), d->code->imp_rows_rec.data(),
+                                d->code->imp_rows_rec.size() * sizeof(uint64_t), hipMemcpyHostToDevice), "I-P upload");
         }
-        d->mcount.reserve(QEC_MC_NCOUNTERS);
+        d->mcount.reserve(QEC_MC_NCOUNTERS_ALL);
     } catch (const std::exception& ex) {
-        (void)hipStreamDestroy(d->stream);
-        delete d;
         fail(QEC_ERR_HIP, std::string("qec_decoder_create: ") + ex.what());
         return nullptr;
     }
-    if (hipEventCreate(&d->ev0) != hipSuccess || hipEventCreate(&d->ev1) != hipSuccess) {
-        (void)hipStreamDestroy(d->stream);
-        delete d;
-        fail(QEC_ERR_HIP, "hipEventCreate failed");
-        return nullptr;
+    return d.release();
+}
+
+qec_decoder* qec_decoder_create_multi(const qec_code* h, const int* devices, int ndevices, size_t max_batch)
+{
+    if (!h || !devices || ndevices <= 0) { fail(QEC_ERR_ARG, "qec_decoder_create_multi: bad argument"); return nullptr; }
+    std::unique_ptr<qec_decoder> g(new (std::nothrow) qec_decoder);
+    if (!g) { fail(QEC_ERR_NOMEM, "qec_decoder_create_multi: out of memory"); return nullptr; }
+    for (int k = 0; k < ndevices; ++k) {
+        qec_decoder* p = qec_decoder_create(h, devices[k], max_batch);
+        if (!p) return nullptr;  // parts created so far are freed with g
+        g->parts.push_back(p);
     }
-    return d;
+    const qec_decoder* p0 = g->parts[0];
+    g->code = p0->code;
+    g->device = p0->device;
+    g->engine = p0->engine;
+    g->variant = p0->variant;
+    std::string name = "multi-device [";
+    for (int k = 0; k < ndevices; ++k) name += (k ? "," : "") + std::to_string(devices[k]);
+    g->variant_name = name + "] " + p0->variant_name;
+    return g.release();
+}
+
+int qec_decoder_num_parts(const qec_decoder* d)
+{
+    if (!d) return fail(QEC_ERR_ARG, "qec_decoder_num_parts: null decoder");
+    return d->parts.empty() ? 1 : (int)d->parts.size();
+}
+
+qec_decoder* qec_decoder_part(qec_decoder* d, int k)
+{
+    if (!d) { fail(QEC_ERR_ARG, "qec_decoder_part: null decoder"); return nullptr; }
+    if (d->parts.empty()) return k == 0 ? d : (fail(QEC_ERR_ARG, "qec_decoder_part: index out of range"), nullptr);
+    if (k < 0 || k >= (int)d->parts.size()) { fail(QEC_ERR_ARG, "qec_decoder_part: index out of range"); return nullptr; }
+    return d->parts[k];
+}
+
+int qec_decoder_device(const qec_decoder* d)
+{
+    if (!d) return fail(QEC_ERR_ARG, "qec_decoder_device: null decoder");
+    return d->device;
 }
 
 int qec_decoder_destroy(qec_decoder* d)
 {
-    if (!d) return QEC_OK;
-    (void)hipSetDevice(d->device);
-    if (d->ev0) (void)hipEventDestroy(d->ev0);
-    if (d->ev1) (void)hipEventDestroy(d->ev1);
-    if (d->stream) (void)hipStreamDestroy(d->stream);
-    if (d->sparse) sparse_plan_free(d->sparse);
     delete d;
     return QEC_OK;
 }
@@ -251,6 +388,10 @@ int qec_decoder_describe(const qec_decoder* d, char* buf, size_t len)
 int qec_decoder_set_option(qec_decoder* d, int option, int value)
 {
     if (!d) return fail(QEC_ERR_ARG, "qec_decoder_set_option: null decoder");
+    for (qec_decoder* p : d->parts) {
+        const int rc = qec_decoder_set_option(p, option, value);
+        if (rc) return rc;
+    }
     switch (option) {
     case QEC_OPT_HARD_PATHS: d->hard_paths = value != 0; return QEC_OK;
     case QEC_OPT_CYCLE_JUMP: d->cycle_jump = value != 0; return QEC_OK;
@@ -261,6 +402,11 @@ int qec_decoder_set_option(qec_decoder* d, int option, int value)
     case QEC_OPT_SECTOR_SPLIT:
         if (value < 0 || value > 2) return fail(QEC_ERR_ARG, "qec_decoder_set_option: QEC_OPT_SECTOR_SPLIT is 0, 1 or 2");
         d->sector_split = value;
+        return QEC_OK;
+    case QEC_OPT_PHASE_STATS:
+        if (value && (!d->variant || !decode_has_phase_stats(d->variant, QEC_STOP_FIXED)))
+            return fail(QEC_ERR_UNSUPPORTED, "qec_decoder_set_option: QEC_OPT_PHASE_STATS needs a shipped code's kernels");
+        d->phase_stats = value != 0;
         return QEC_OK;
     default: return fail(QEC_ERR_ARG, "qec_decoder_set_option: unknown option");
     }
@@ -274,95 +420,195 @@ int qec_decoder_get_option(const qec_decoder* d, int option, int* value)
     case QEC_OPT_CYCLE_JUMP: *value = d->cycle_jump; return QEC_OK;
     case QEC_OPT_SCHEDULE: *value = d->schedule; return QEC_OK;
     case QEC_OPT_SECTOR_SPLIT: *value = d->sector_split; return QEC_OK;
+    case QEC_OPT_PHASE_STATS: *value = d->phase_stats; return QEC_OK;
     default: return fail(QEC_ERR_ARG, "qec_decoder_get_option: unknown option");
     }
 }
 
-// QEC_OPT_SCHEDULE = 1 orders batches from this size on (below it the three extra launches
+}  // extern "C"
+
+namespace {
+
+// QEC_OPT_SCHEDULE = 1 orders batches from this size on (below it the two extra launches
 // cost more than the tail they remove)
 constexpr long long kScheduleMinBatch = 4096;
 
-static int dispatch_decode(qec_decoder* d, const uint8_t* sX, const uint8_t* sZ, long long B, float p, int maxIter,
-                           int stop, uint8_t* eX, uint8_t* eZ, uint8_t* flags, int32_t* iters, float* q, hipStream_t st)
+// One decode launch of a single-device handle on device buffers.  Outputs: byte form (eX, eZ,
+// flags) or, with rec non-null, the packed decision records.
+int dispatch_decode(qec_decoder* d, const uint8_t* sX, const uint8_t* sZ, long long B, float p, int maxIter, int stop,
+                    uint8_t* eX, uint8_t* eZ, uint8_t* flags, uint8_t* rec, int32_t* iters, float* q, hipStream_t st)
 {
-    if (d->engine == QEC_ENGINE_SPARSE)
-        return launch_decode_sparse(d->sparse, sX, sZ, B, p, maxIter, stop, eX, eZ, flags, iters, q, st);
-    const int hp = d->hard_paths ? (QEC_HP_FORMS | (d->cycle_jump ? QEC_HP_CYCLE : 0)) : 0;
+    if (B <= 0) return QEC_OK;
+    const Code& c = *d->code;
+    int rc = ws_acquire(d, st);
+    if (rc) return rc;
+    if (d->engine == QEC_ENGINE_SPARSE) {
+        if (rec != nullptr) {  // byte outputs into the handle's staging, then packed
+            if ((rc = ws_reserve(d->eX, (size_t)B * c.n, st, "decode")) || (rc = ws_reserve(d->eZ, (size_t)B * c.n, st, "decode")) ||
+                (rc = ws_reserve(d->flags, (size_t)B, st, "decode")))
+                return rc;
+            eX = d->eX.data(); eZ = d->eZ.data(); flags = d->flags.data();
+        }
+        rc = launch_decode_sparse(d->sparse, sX, sZ, B, p, maxIter, stop, eX, eZ, flags, iters, q, st);
+        if (!rc && rec != nullptr) rc = launch_pack_decisions(eX, eZ, flags, B, c.n, rec, st);
+        if (rc) return rc;
+        return ws_release(d, st);
+    }
+    const int hp = (d->hard_paths ? (QEC_HP_FORMS | (d->cycle_jump ? QEC_HP_CYCLE : 0)) : 0) |
+                   (d->phase_stats ? QEC_HP_PHASE : 0);
+    const bool split = !d->phase_stats && decode_uses_split(d->variant, stop, d->sector_split);
+    if (split && (rc = ws_reserve(d->merge, (size_t)B, st, "decode"))) return rc;
     const int32_t* perm = nullptr;
     bool zeroed = false;
     if (B > 1 && B <= schedule_max_batch() && (d->schedule == 2 || (d->schedule == 1 && B >= kScheduleMinBatch))) {
-        try {
-            d->sched.reserve(schedule_workspace_bytes(B, d->code->mX, d->code->mZ));
-        } catch (const std::exception& ex) {
-            return fail(QEC_ERR_NOMEM, std::string("decode: dispatch-order workspace: ") + ex.what());
-        }
-        // a sector-split launch ORs its flags into a zeroed array: the order pass zeroes it
-        zeroed = decode_uses_split(d->variant, stop, d->sector_split);
+        if ((rc = ws_reserve(d->sched, schedule_workspace_bytes(B, c.mX, c.mZ), st, "decode: dispatch order")))
+            return rc;
         int32_t* pm = nullptr;
-        const int rc = launch_schedule(sX, sZ, B, d->code->mX, d->code->mZ, d->sched.data(), zeroed ? flags : nullptr,
-                                       &pm, st);
+        // a sector-split launch merges its flags in zeroed words: the order pass zeroes them
+        rc = launch_schedule(sX, sZ, B, c.mX, c.mZ, d->sched.data(), split ? d->merge.data() : nullptr, &pm, st);
         if (rc) return rc;
         perm = pm;
+        zeroed = split;
     }
-    return launch_decode(d->variant, *d->code, sX, sZ, B, p, maxIter, stop, eX, eZ, flags, iters, q, hp, perm,
-                         d->sector_split, zeroed, st);
+    rc = launch_decode(d->variant, c, sX, sZ, B, p, maxIter, stop, eX, eZ, flags, rec, iters, q, hp, perm,
+                       d->sector_split, split ? d->merge.data() : nullptr, zeroed, st);
+    if (rc) return rc;
+    return ws_release(d, st);
 }
 
-static const int32_t* syndrome_table(const qec_decoder* d)
+const int32_t* syndrome_table(const qec_decoder* d)
 {
     return d->engine == QEC_ENGINE_SPARSE ? sparse_plan_chkvar(d->sparse) : nullptr;
 }
 
-static int check_decode_args(const qec_decoder* d, const void* sX, const void* sZ, size_t B, int stop,
-                             const void* eX, const void* eZ, const void* flags)
+int check_decode_args(const qec_decoder* d, const void* sX, const void* sZ, size_t B, int stop)
 {
     if (!d) return fail(QEC_ERR_ARG, "decode: null decoder");
     if (stop < QEC_STOP_REF || stop > QEC_STOP_SYNDROME) return fail(QEC_ERR_ARG, "decode: unknown stop rule");
-    if (B && (!sX || !sZ || !eX || !eZ || !flags)) return fail(QEC_ERR_ARG, "decode: null buffer");
+    if (B && (!sX || !sZ)) return fail(QEC_ERR_ARG, "decode: null syndrome buffer");
     if (B > (size_t)1 << 40) return fail(QEC_ERR_ARG, "decode: batch too large");
     return QEC_OK;
 }
 
+int single_device_only(const qec_decoder* d, const char* what)
+{
+    if (!d->parts.empty())
+        return fail(QEC_ERR_ARG, std::string(what) + ": device buffers live on one GPU; call it on a part "
+                                                     "(qec_decoder_part) of a multi-device decoder");
+    return QEC_OK;
+}
+
+// Host-buffer decode of one single-device handle (synchronous): stage, decode, copy back.
+int decode_host(qec_decoder* d, const uint8_t* sX, const uint8_t* sZ, size_t B, float p, int maxIter, int stop,
+                uint8_t* eX, uint8_t* eZ, uint8_t* flags, uint8_t* rec, int32_t* iters, float* q)
+{
+    if (B == 0) return QEC_OK;
+    QEC_DEVICE_SCOPE(d->device);
+    const Code& c = *d->code;
+    const size_t qn = (size_t)(c.mX + c.mZ) * c.L;
+    const size_t recB = 2 * (size_t)((c.n + 7) / 8) + 1;
+    hipStream_t st = d->stream;
+    try {
+        d->sX.reserve(B * c.mX); d->sZ.reserve(B * c.mZ);
+        if (rec) d->rec.reserve(B * recB);
+        else { d->eX.reserve(B * c.n); d->eZ.reserve(B * c.n); d->flags.reserve(B); }
+        if (iters) d->iters.reserve(2 * B);
+        if (q) d->q.reserve(B * qn);
+    } catch (const std::exception& ex) {
+        return fail(QEC_ERR_HIP, std::string("device staging allocation: ") + ex.what());
+    }
+    QEC_HIP_CHECK(hipMemcpyAsync(d->sX.data(), sX, B * c.mX, hipMemcpyHostToDevice, st));
+    QEC_HIP_CHECK(hipMemcpyAsync(d->sZ.data(), sZ, B * c.mZ, hipMemcpyHostToDevice, st));
+    // the sparse engine's packed path stages its byte outputs in eX/eZ/flags (dispatch_decode)
+    int rc = dispatch_decode(d, d->sX.data(), d->sZ.data(), (long long)B, p, maxIter, stop, rec ? nullptr : d->eX.data(),
+                             rec ? nullptr : d->eZ.data(), rec ? nullptr : d->flags.data(), rec ? d->rec.data() : nullptr,
+                             iters ? d->iters.data() : nullptr, q ? d->q.data() : nullptr, st);
+    if (rc) return rc;
+    if (rec) {
+        QEC_HIP_CHECK(hipMemcpyAsync(rec, d->rec.data(), B * recB, hipMemcpyDeviceToHost, st));
+    } else {
+        QEC_HIP_CHECK(hipMemcpyAsync(eX, d->eX.data(), B * c.n, hipMemcpyDeviceToHost, st));
+        QEC_HIP_CHECK(hipMemcpyAsync(eZ, d->eZ.data(), B * c.n, hipMemcpyDeviceToHost, st));
+        QEC_HIP_CHECK(hipMemcpyAsync(flags, d->flags.data(), B, hipMemcpyDeviceToHost, st));
+    }
+    if (iters) QEC_HIP_CHECK(hipMemcpyAsync(iters, d->iters.data(), 2 * B * sizeof(int32_t), hipMemcpyDeviceToHost, st));
+    if (q) QEC_HIP_CHECK(hipMemcpyAsync(q, d->q.data(), B * qn * sizeof(float), hipMemcpyDeviceToHost, st));
+    QEC_HIP_CHECK(hipStreamSynchronize(st));
+    return QEC_OK;
+}
+
+// Host-buffer decode on every part of a handle: contiguous shards, one host thread per part
+// (the reference's sample-parallel loop, DecoderCPU.h:419-438, across devices).
+int decode_host_parts(qec_decoder* d, const uint8_t* sX, const uint8_t* sZ, size_t B, float p, int maxIter, int stop,
+                      uint8_t* eX, uint8_t* eZ, uint8_t* flags, uint8_t* rec, int32_t* iters, float* q)
+{
+    const std::vector<qec_decoder*> parts = parts_of(d);
+    if (parts.size() == 1)
+        return decode_host(parts[0], sX, sZ, B, p, maxIter, stop, eX, eZ, flags, rec, iters, q);
+    const Code& c = *d->code;
+    const size_t qn = (size_t)(c.mX + c.mZ) * c.L;
+    const size_t recB = 2 * (size_t)((c.n + 7) / 8) + 1;
+    const int np = (int)parts.size();
+    std::vector<int> rcs(np, QEC_OK);
+    std::vector<std::string> errs(np);
+    std::vector<std::thread> th;
+    for (int k = 0; k < np; ++k) {
+        const size_t lo = (size_t)shard_lo((long long)B, k, np), hi = (size_t)shard_lo((long long)B, k + 1, np);
+        th.emplace_back([&, k, lo, hi] {
+            rcs[k] = decode_host(parts[k], sX + lo * c.mX, sZ + lo * c.mZ, hi - lo, p, maxIter, stop,
+                                 eX ? eX + lo * c.n : nullptr, eZ ? eZ + lo * c.n : nullptr, flags ? flags + lo : nullptr,
+                                 rec ? rec + lo * recB : nullptr, iters ? iters + 2 * lo : nullptr, q ? q + lo * qn : nullptr);
+            if (rcs[k]) errs[k] = last_error_cstr();
+        });
+    }
+    for (auto& t : th) t.join();
+    for (int k = 0; k < np; ++k)
+        if (rcs[k]) return fail(rcs[k], "part " + std::to_string(k) + ": " + errs[k]);
+    return QEC_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
 int qec_decode_batch_dev(qec_decoder* d, const uint8_t* sX, const uint8_t* sZ, size_t B, float p, int maxIter,
                          int stop, uint8_t* eX, uint8_t* eZ, uint8_t* flags, int32_t* iters, float* q, void* stream)
 {
-    int rc = check_decode_args(d, sX, sZ, B, stop, eX, eZ, flags);
-    if (rc) return rc;
-    QEC_HIP_CHECK(hipSetDevice(d->device));
-    return dispatch_decode(d, sX, sZ, (long long)B, p, maxIter, stop, eX, eZ, flags, iters, q,
+    int rc = check_decode_args(d, sX, sZ, B, stop);
+    if (rc || (rc = single_device_only(d, "qec_decode_batch_dev"))) return rc;
+    if (B && (!eX || !eZ || !flags)) return fail(QEC_ERR_ARG, "decode: null output buffer");
+    QEC_DEVICE_SCOPE(d->device);
+    return dispatch_decode(d, sX, sZ, (long long)B, p, maxIter, stop, eX, eZ, flags, nullptr, iters, q,
+                           static_cast<hipStream_t>(stream));
+}
+
+int qec_decode_batch_packed_dev(qec_decoder* d, const uint8_t* sX, const uint8_t* sZ, size_t B, float p, int maxIter,
+                                int stop, uint8_t* records, int32_t* iters, float* q, void* stream)
+{
+    int rc = check_decode_args(d, sX, sZ, B, stop);
+    if (rc || (rc = single_device_only(d, "qec_decode_batch_packed_dev"))) return rc;
+    if (B && !records) return fail(QEC_ERR_ARG, "decode: null record buffer");
+    QEC_DEVICE_SCOPE(d->device);
+    return dispatch_decode(d, sX, sZ, (long long)B, p, maxIter, stop, nullptr, nullptr, nullptr, records, iters, q,
                            static_cast<hipStream_t>(stream));
 }
 
 int qec_decode_batch(qec_decoder* d, const uint8_t* sX, const uint8_t* sZ, size_t B, float p, int maxIter, int stop,
                      uint8_t* eX, uint8_t* eZ, uint8_t* flags, int32_t* iters, float* q)
 {
-    int rc = check_decode_args(d, sX, sZ, B, stop, eX, eZ, flags);
+    int rc = check_decode_args(d, sX, sZ, B, stop);
     if (rc) return rc;
-    if (B == 0) return QEC_OK;
-    QEC_HIP_CHECK(hipSetDevice(d->device));
-    const Code& c = *d->code;
-    const size_t qn = (size_t)(c.mX + c.mZ) * c.L;
-    try {
-        d->sX.reserve(B * c.mX); d->sZ.reserve(B * c.mZ);
-        d->eX.reserve(B * c.n); d->eZ.reserve(B * c.n); d->flags.reserve(B);
-        if (iters) d->iters.reserve(2 * B);
-        if (q) d->q.reserve(B * qn);
-    } catch (const std::exception& ex) {
-        return fail(QEC_ERR_HIP, std::string("device staging allocation: ") + ex.what());
-    }
-    hipStream_t st = d->stream;
-    QEC_HIP_CHECK(hipMemcpyAsync(d->sX.data(), sX, B * c.mX, hipMemcpyHostToDevice, st));
-    QEC_HIP_CHECK(hipMemcpyAsync(d->sZ.data(), sZ, B * c.mZ, hipMemcpyHostToDevice, st));
-    rc = dispatch_decode(d, d->sX.data(), d->sZ.data(), (long long)B, p, maxIter, stop, d->eX.data(),
-                       d->eZ.data(), d->flags.data(), iters ? d->iters.data() : nullptr, q ? d->q.data() : nullptr, st);
+    if (B && (!eX || !eZ || !flags)) return fail(QEC_ERR_ARG, "decode: null output buffer");
+    return decode_host_parts(d, sX, sZ, B, p, maxIter, stop, eX, eZ, flags, nullptr, iters, q);
+}
+
+int qec_decode_batch_packed(qec_decoder* d, const uint8_t* sX, const uint8_t* sZ, size_t B, float p, int maxIter,
+                            int stop, uint8_t* records, int32_t* iters)
+{
+    int rc = check_decode_args(d, sX, sZ, B, stop);
     if (rc) return rc;
-    QEC_HIP_CHECK(hipMemcpyAsync(eX, d->eX.data(), B * c.n, hipMemcpyDeviceToHost, st));
-    QEC_HIP_CHECK(hipMemcpyAsync(eZ, d->eZ.data(), B * c.n, hipMemcpyDeviceToHost, st));
-    QEC_HIP_CHECK(hipMemcpyAsync(flags, d->flags.data(), B, hipMemcpyDeviceToHost, st));
-    if (iters) QEC_HIP_CHECK(hipMemcpyAsync(iters, d->iters.data(), 2 * B * sizeof(int32_t), hipMemcpyDeviceToHost, st));
-    if (q) QEC_HIP_CHECK(hipMemcpyAsync(q, d->q.data(), B * qn * sizeof(float), hipMemcpyDeviceToHost, st));
-    QEC_HIP_CHECK(hipStreamSynchronize(st));
-    return QEC_OK;
+    if (B && !records) return fail(QEC_ERR_ARG, "decode: null record buffer");
+    return decode_host_parts(d, sX, sZ, B, p, maxIter, stop, nullptr, nullptr, nullptr, records, iters, nullptr);
 }
 
 int qec_sample_fixed_weight(uint32_t seed, int W, size_t count, int n, uint8_t* x, uint8_t* z)
@@ -381,42 +627,117 @@ int qec_sample_fixed_weight(uint32_t seed, int W, size_t count, int n, uint8_t* 
     return QEC_OK;
 }
 
-static void mc_reserve(qec_decoder* d, size_t B, int W)
-{
-    const Code& c = *d->code;
-    d->mx.reserve(B * c.n); d->mz.reserve(B * c.n);
-    d->msX.reserve(B * c.mX); d->msZ.reserve(B * c.mZ);
-    d->meX.reserve(B * c.n); d->meZ.reserve(B * c.n);
-    d->mfl.reserve(B); d->mit.reserve(2 * B);
-    if (W > 0) { d->midx.reserve(B * W); d->mtype.reserve(B * W); }
-}
+}  // extern "C"
 
-// decode + statistics of the batch already in d->mx / d->mz; adds decode time
-static int mc_decode_and_count(qec_decoder* d, long long B, float p, int maxIter, int stop, double& decode_s)
+namespace {
+
+// Monte-Carlo workspace of one part for batches of up to B samples (W draws each).
+int mc_reserve(qec_decoder* d, size_t B, int W)
 {
     const Code& c = *d->code;
-    hipStream_t st = d->stream;
-    int rc = launch_syndrome(c, syndrome_table(d), d->mx.data(), d->mz.data(), B, d->msX.data(), d->msZ.data(), st);
-    if (rc) return rc;
-    QEC_HIP_CHECK(hipEventRecord(d->ev0, st));
-    rc = dispatch_decode(d, d->msX.data(), d->msZ.data(), B, p, maxIter, stop, d->meX.data(), d->meZ.data(),
-                       d->mfl.data(), d->mit.data(), nullptr, st);
-    if (rc) return rc;
-    QEC_HIP_CHECK(hipEventRecord(d->ev1, st));
-    rc = launch_statistics(c, d->imp.data(), d->mx.data(), d->mz.data(), d->meX.data(), d->meZ.data(), d->mfl.data(), B,
-                           d->mcount.data(), st);
-    if (rc) return rc;
-    QEC_HIP_CHECK(hipEventSynchronize(d->ev1));
-    float ms = 0;
-    QEC_HIP_CHECK(hipEventElapsedTime(&ms, d->ev0, d->ev1));
-    decode_s += ms * 1e-3;
+    const size_t nb = (size_t)(c.n + 7) / 8;
+    try {
+        d->msX.reserve(B * c.mX); d->msZ.reserve(B * c.mZ);
+        d->merrp.reserve(B * 2 * nb); d->mrec.reserve(B * (2 * nb + 1));
+        d->mit.reserve(2 * B);
+        if (W > 0) { d->midx.reserve(B * W); d->mtype.reserve(B * W); }
+    } catch (const std::exception& ex) {
+        return fail(QEC_ERR_HIP, std::string("Monte-Carlo workspace: ") + ex.what());
+    }
     return QEC_OK;
 }
 
+// errors (source filled in h by the caller) -> syndromes + packed errors -> packed decode ->
+// counters, all enqueued on the part's stream
+int mc_batch(qec_decoder* d, McArgsHost h, int src, float p, int maxIter, int stop, bool want_iters,
+             hipEvent_t ev0, hipEvent_t ev1)
+{
+    hipStream_t st = d->stream;
+    h.code = d->code.get();
+    h.sX = d->msX.data(); h.sZ = d->msZ.data(); h.errp = d->merrp.data();
+    h.chkVar = syndrome_table(d);
+    int rc = launch_mc_errors_syndrome(src, h, st);
+    if (rc) return rc;
+    if (ev0) QEC_HIP_CHECK(hipEventRecord(ev0, st));
+    rc = dispatch_decode(d, d->msX.data(), d->msZ.data(), h.B, p, maxIter, stop, nullptr, nullptr, nullptr,
+                         d->mrec.data(), want_iters ? d->mit.data() : nullptr, nullptr, st);
+    if (rc) return rc;
+    if (ev1) QEC_HIP_CHECK(hipEventRecord(ev1, st));
+    return launch_statistics_packed(*d->code, d->imp_rec.data(), d->merrp.data(), d->mrec.data(),
+                                    want_iters ? d->mit.data() : nullptr, h.B, d->mcount.data(), st);
+}
+
+int mc_fetch_counters(qec_decoder* d, unsigned long long* out)
+{
+    QEC_HIP_CHECK(hipMemcpyAsync(out, d->mcount.data(), QEC_MC_NCOUNTERS_ALL * sizeof(unsigned long long),
+                                 hipMemcpyDeviceToHost, d->stream));
+    QEC_HIP_CHECK(hipStreamSynchronize(d->stream));
+    return QEC_OK;
+}
+
+struct EventSet {
+    std::vector<hipEvent_t> ev;
+    ~EventSet()
+    {
+        for (hipEvent_t e : ev) (void)hipEventDestroy(e);
+    }
+    int make(size_t n, unsigned flags)
+    {
+        ev.assign(n, nullptr);
+        for (auto& e : ev) QEC_HIP_CHECK(hipEventCreateWithFlags(&e, flags));
+        return QEC_OK;
+    }
+};
+
+// qec_monte_carlo on one part: samples [start, start + count), counters left in d->mcount
+int monte_carlo_part(qec_decoder* d, uint64_t seed, uint64_t start, uint64_t count, float p, int maxIter, int stop,
+                     size_t batch, double* decode_s)
+{
+    QEC_DEVICE_SCOPE(d->device);
+    hipStream_t st = d->stream;
+    int rc = mc_reserve(d, (size_t)std::min<uint64_t>(batch, std::max<uint64_t>(count, 1)), 0);
+    if (rc) return rc;
+    QEC_HIP_CHECK(hipMemsetAsync(d->mcount.data(), 0, QEC_MC_NCOUNTERS_ALL * sizeof(unsigned long long), st));
+    // decode-kernel time from a ring of event pairs: the host waits only on a pair it reuses,
+    // kRing batches behind the launches (no per-batch synchronisation)
+    constexpr size_t kRing = 32;
+    EventSet ev;
+    if ((rc = ev.make(2 * kRing, hipEventDefault))) return rc;
+    double dec = 0;
+    uint64_t k = 0;
+    auto harvest = [&](size_t slot) -> int {
+        QEC_HIP_CHECK(hipEventSynchronize(ev.ev[2 * slot + 1]));
+        float ms = 0;
+        QEC_HIP_CHECK(hipEventElapsedTime(&ms, ev.ev[2 * slot], ev.ev[2 * slot + 1]));
+        dec += ms * 1e-3;
+        return QEC_OK;
+    };
+    for (uint64_t base = 0; base < count; base += batch, ++k) {
+        const size_t slot = k % kRing;
+        if (k >= kRing && (rc = harvest(slot))) return rc;
+        McArgsHost h;
+        h.seed = seed; h.start = start + base; h.p = p;
+        h.B = (long long)std::min<uint64_t>(batch, count - base);
+        rc = mc_batch(d, h, MC_SRC_PHILOX, p, maxIter, stop, true, ev.ev[2 * slot], ev.ev[2 * slot + 1]);
+        if (rc) return rc;
+    }
+    for (uint64_t j = k > kRing ? k - kRing : 0; j < k; ++j)
+        if ((rc = harvest(j % kRing))) return rc;
+    *decode_s = dec;
+    return QEC_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
 // GetStatistics (DecoderCPU.h:392-530).  The errors are the reference's: W (index, type) draws
 // per sample from one mt19937(seed) stream through VS2015's uniform_int_distribution, drawn on
-// the host in sample order (the stream is sequential).  Everything after the draws runs on the
-// GPU: error expansion, syndromes, decode (reference stop rule), I-P check, counters.
+// the host in sample order (the stream is sequential), into a double-buffered pinned chunk so the
+// next chunk is drawn while the devices work on this one.  Each chunk is sharded contiguously
+// over the decoder's parts; on each device: errors from the draws + syndromes + packed errors
+// (one fused launch), decode (reference stop rule) to packed records, I-P check and counters.
+// The counters do not depend on the sample order, so the per-device sums add up exactly.
 int qec_get_statistics(qec_decoder* d, int W, int numErrors, float p, int maxIter, uint32_t seed, int nThreads,
                        qec_stats* out)
 {
@@ -424,44 +745,71 @@ int qec_get_statistics(qec_decoder* d, int W, int numErrors, float p, int maxIte
     const Code& c = *d->code;
     if (c.imp.empty()) return fail(QEC_ERR_UNSUPPORTED, "qec_get_statistics: code has no I-P matrix for the logical check");
     if (nThreads < 1) nThreads = 1;
-    QEC_HIP_CHECK(hipSetDevice(d->device));
     const auto t0 = std::chrono::high_resolution_clock::now();
     const long tested = (long)(numErrors / nThreads) * nThreads;  // DecoderCPU.h:426,527
     const long CH = 1 << 16;
     const int n = c.n;
-    hipStream_t st = d->stream;
+    const std::vector<qec_decoder*> parts = parts_of(d);
+    const int np = (int)parts.size();
+    const long cap = std::max<long>(1, (std::min<long>(CH, std::max<long>(tested, 1)) + np - 1) / np);
+    std::vector<EventSet> consumed(2 * np);  // [buffer][part]: the part's copy out of the pinned buffer is done
+    for (int j = 0; j < np; ++j) {
+        QEC_DEVICE_SCOPE(parts[j]->device);
+        int rc = mc_reserve(parts[j], (size_t)cap, W);
+        if (rc) return rc;
+        QEC_HIP_CHECK(hipMemsetAsync(parts[j]->mcount.data(), 0, QEC_MC_NCOUNTERS_ALL * sizeof(unsigned long long),
+                                     parts[j]->stream));
+        for (int k = 0; k < 2; ++k)
+            if ((rc = consumed[k * np + j].make(1, hipEventDisableTiming))) return rc;
+    }
+    const size_t draws = (size_t)std::min<long>(CH, std::max<long>(tested, 1)) * std::max(W, 1);
+    PinnedArray<int32_t> hidx[2];
+    PinnedArray<uint8_t> htype[2];
     try {
-        mc_reserve(d, (size_t)std::min<long>(CH, std::max<long>(tested, 1)), W);
+        for (int k = 0; k < 2; ++k) { hidx[k].reserve(draws); htype[k].reserve(draws); }
     } catch (const std::exception& ex) {
         return fail(QEC_ERR_HIP, std::string("qec_get_statistics: ") + ex.what());
     }
-    QEC_HIP_CHECK(hipMemsetAsync(d->mcount.data(), 0, QEC_MC_NCOUNTERS * sizeof(unsigned long long), st));
-    PinnedArray<int32_t> hidx;
-    PinnedArray<uint8_t> htype;
-    hidx.reserve((size_t)std::min<long>(CH, std::max<long>(tested, 1)) * std::max(W, 1));
-    htype.reserve((size_t)std::min<long>(CH, std::max<long>(tested, 1)) * std::max(W, 1));
     Mt19937 g(seed);
-    double dec_s = 0;
-    for (long base = 0; base < tested; base += CH) {
+    long chunk = 0;
+    for (long base = 0; base < tested; base += CH, ++chunk) {
+        const int k = (int)(chunk & 1);
         const long cnt = std::min(CH, tested - base);
+        if (chunk >= 2)
+            for (int j = 0; j < np; ++j) QEC_HIP_CHECK(hipEventSynchronize(consumed[k * np + j].ev[0]));
         for (long s = 0; s < cnt; ++s)
             for (int w = 0; w < W; ++w) {
-                hidx[s * W + w] = (int32_t)g.msvc_uniform((uint32_t)n);  // index, then type (DecoderCPU.h:452-454)
-                htype[s * W + w] = (uint8_t)g.msvc_uniform(3u);
+                hidx[k][s * W + w] = (int32_t)g.msvc_uniform((uint32_t)n);  // index, then type (DecoderCPU.h:452-454)
+                htype[k][s * W + w] = (uint8_t)g.msvc_uniform(3u);
             }
-        if (W > 0) {
-            QEC_HIP_CHECK(hipMemcpyAsync(d->midx.data(), hidx.data(), (size_t)cnt * W * sizeof(int32_t),
-                                         hipMemcpyHostToDevice, st));
-            QEC_HIP_CHECK(hipMemcpyAsync(d->mtype.data(), htype.data(), (size_t)cnt * W, hipMemcpyHostToDevice, st));
+        for (int j = 0; j < np; ++j) {
+            qec_decoder* pd = parts[j];
+            const long lo = (long)shard_lo(cnt, j, np), hi = (long)shard_lo(cnt, j + 1, np);
+            if (hi == lo) continue;
+            QEC_DEVICE_SCOPE(pd->device);
+            hipStream_t st = pd->stream;
+            if (W > 0) {
+                QEC_HIP_CHECK(hipMemcpyAsync(pd->midx.data(), hidx[k].data() + (size_t)lo * W,
+                                             (size_t)(hi - lo) * W * sizeof(int32_t), hipMemcpyHostToDevice, st));
+                QEC_HIP_CHECK(hipMemcpyAsync(pd->mtype.data(), htype[k].data() + (size_t)lo * W, (size_t)(hi - lo) * W,
+                                             hipMemcpyHostToDevice, st));
+            }
+            QEC_HIP_CHECK(hipEventRecord(consumed[k * np + j].ev[0], st));
+            McArgsHost h;
+            h.idx = pd->midx.data(); h.type = pd->mtype.data(); h.W = W;
+            h.B = hi - lo;
+            const int rc = mc_batch(pd, h, MC_SRC_DRAWS, p, maxIter, QEC_STOP_REF, false, nullptr, nullptr);
+            if (rc) return rc;
         }
-        int rc = launch_errors_from_draws(d->midx.data(), d->mtype.data(), cnt, W, n, d->mx.data(), d->mz.data(), st);
-        if (rc) return rc;
-        rc = mc_decode_and_count(d, cnt, p, maxIter, QEC_STOP_REF, dec_s);
-        if (rc) return rc;
     }
-    unsigned long long cn[QEC_MC_NCOUNTERS];
-    QEC_HIP_CHECK(hipMemcpyAsync(cn, d->mcount.data(), sizeof cn, hipMemcpyDeviceToHost, st));
-    QEC_HIP_CHECK(hipStreamSynchronize(st));
+    unsigned long long cn[QEC_MC_NCOUNTERS_ALL] = {};
+    for (qec_decoder* pd : parts) {
+        QEC_DEVICE_SCOPE(pd->device);
+        unsigned long long part[QEC_MC_NCOUNTERS_ALL];
+        const int rc = mc_fetch_counters(pd, part);
+        if (rc) return rc;
+        for (int k = 0; k < QEC_MC_NCOUNTERS_ALL; ++k) cn[k] += part[k];
+    }
     const auto t1 = std::chrono::high_resolution_clock::now();
     std::memset(out, 0, sizeof *out);
     out->randSeed = seed;
@@ -479,20 +827,89 @@ int qec_get_statistics(qec_decoder* d, int W, int numErrors, float p, int maxIte
     return QEC_OK;
 }
 
+int qec_monte_carlo(qec_decoder* d, uint64_t seed, uint64_t start, uint64_t count, float p, int maxIter, int stop,
+                    size_t batch, qec_mc_result* out)
+{
+    if (!d || !out || (stop < QEC_STOP_REF || stop > QEC_STOP_SYNDROME)) return fail(QEC_ERR_ARG, "qec_monte_carlo: bad argument");
+    const Code& c = *d->code;
+    if (c.imp.empty()) return fail(QEC_ERR_UNSUPPORTED, "qec_monte_carlo: code has no I-P matrix for the logical check");
+    if (batch == 0) batch = 65536;
+    const auto t0 = std::chrono::high_resolution_clock::now();
+    const std::vector<qec_decoder*> parts = parts_of(d);
+    const int np = (int)parts.size();
+    std::vector<int> rcs(np, QEC_OK);
+    std::vector<std::string> errs(np);
+    std::vector<double> dec(np, 0.0);
+    std::vector<std::thread> th;
+    for (int j = 0; j < np; ++j) {
+        const uint64_t lo = (uint64_t)shard_lo((long long)count, j, np), hi = (uint64_t)shard_lo((long long)count, j + 1, np);
+        th.emplace_back([&, j, lo, hi] {
+            rcs[j] = monte_carlo_part(parts[j], seed, start + lo, hi - lo, p, maxIter, stop, batch, &dec[j]);
+            if (rcs[j]) errs[j] = last_error_cstr();
+        });
+    }
+    for (auto& t : th) t.join();
+    unsigned long long cn[QEC_MC_NCOUNTERS_ALL] = {};
+    for (int j = 0; j < np; ++j) {
+        if (rcs[j]) return fail(rcs[j], "part " + std::to_string(j) + ": " + errs[j]);
+        QEC_DEVICE_SCOPE(parts[j]->device);
+        unsigned long long part[QEC_MC_NCOUNTERS_ALL];
+        const int rc = mc_fetch_counters(parts[j], part);
+        if (rc) return rc;
+        for (int k = 0; k < QEC_MC_NCOUNTERS_ALL; ++k) cn[k] += part[k];
+    }
+    const auto t1 = std::chrono::high_resolution_clock::now();
+    out->tested = count;
+    out->withX = cn[QEC_MC_WITHX]; out->withZ = cn[QEC_MC_WITHZ];
+    out->synX = cn[QEC_MC_SYNX]; out->synZ = cn[QEC_MC_SYNZ];
+    out->logical = cn[QEC_MC_LOGICAL]; out->corrected = cn[QEC_MC_CORRECTED];
+    out->convX = cn[QEC_MC_CONVX]; out->convZ = cn[QEC_MC_CONVZ];
+    out->iterationsX = cn[QEC_MC_ITERX]; out->iterationsZ = cn[QEC_MC_ITERZ];
+    out->decodeSeconds = *std::max_element(dec.begin(), dec.end());
+    out->totalSeconds = std::chrono::duration<double>(t1 - t0).count();
+    return QEC_OK;
+}
+
 int qec_sample_depolarizing_dev(qec_decoder* d, uint64_t seed, uint64_t start, size_t B, float p, uint8_t* x,
                                 uint8_t* z, void* stream)
 {
     if (!d || (B && (!x || !z))) return fail(QEC_ERR_ARG, "qec_sample_depolarizing_dev: bad argument");
-    QEC_HIP_CHECK(hipSetDevice(d->device));
+    int rc = single_device_only(d, "qec_sample_depolarizing_dev");
+    if (rc) return rc;
+    QEC_DEVICE_SCOPE(d->device);
     return launch_sample_depolarizing(seed, start, (long long)B, d->code->n, p, x, z, static_cast<hipStream_t>(stream));
+}
+
+int qec_sample_syndrome_dev(qec_decoder* d, uint64_t seed, uint64_t start, size_t B, float p, uint8_t* sX, uint8_t* sZ,
+                            uint8_t* errp, void* stream)
+{
+    if (!d || (B && (!sX || !sZ))) return fail(QEC_ERR_ARG, "qec_sample_syndrome_dev: bad argument");
+    int rc = single_device_only(d, "qec_sample_syndrome_dev");
+    if (rc) return rc;
+    QEC_DEVICE_SCOPE(d->device);
+    McArgsHost h;
+    h.code = d->code.get();
+    h.seed = seed; h.start = start; h.p = p;
+    h.sX = sX; h.sZ = sZ; h.errp = errp;
+    h.chkVar = syndrome_table(d);
+    h.B = (long long)B;
+    return launch_mc_errors_syndrome(MC_SRC_PHILOX, h, static_cast<hipStream_t>(stream));
 }
 
 int qec_syndrome_dev(qec_decoder* d, const uint8_t* x, const uint8_t* z, size_t B, uint8_t* sX, uint8_t* sZ,
                      void* stream)
 {
     if (!d || (B && (!x || !z || !sX || !sZ))) return fail(QEC_ERR_ARG, "qec_syndrome_dev: bad argument");
-    QEC_HIP_CHECK(hipSetDevice(d->device));
-    return launch_syndrome(*d->code, syndrome_table(d), x, z, (long long)B, sX, sZ, static_cast<hipStream_t>(stream));
+    int rc = single_device_only(d, "qec_syndrome_dev");
+    if (rc) return rc;
+    QEC_DEVICE_SCOPE(d->device);
+    McArgsHost h;
+    h.code = d->code.get();
+    h.x = x; h.z = z;
+    h.sX = sX; h.sZ = sZ;
+    h.chkVar = syndrome_table(d);
+    h.B = (long long)B;
+    return launch_mc_errors_syndrome(MC_SRC_BYTES, h, static_cast<hipStream_t>(stream));
 }
 
 int qec_pack_decisions_dev(qec_decoder* d, const uint8_t* eX, const uint8_t* eZ, const uint8_t* flags, size_t B,
@@ -500,7 +917,9 @@ int qec_pack_decisions_dev(qec_decoder* d, const uint8_t* eX, const uint8_t* eZ,
 {
     if (!d || (B && (!eX || !eZ || !flags || !out))) return fail(QEC_ERR_ARG, "qec_pack_decisions_dev: bad argument");
     if (B > (size_t)1 << 36) return fail(QEC_ERR_ARG, "qec_pack_decisions_dev: batch too large");
-    QEC_HIP_CHECK(hipSetDevice(d->device));
+    int rc = single_device_only(d, "qec_pack_decisions_dev");
+    if (rc) return rc;
+    QEC_DEVICE_SCOPE(d->device);
     return launch_pack_decisions(eX, eZ, flags, (long long)B, d->code->n, out, static_cast<hipStream_t>(stream));
 }
 
@@ -510,54 +929,23 @@ int qec_statistics_dev(qec_decoder* d, const uint8_t* x, const uint8_t* z, const
     if (!d || !counters || (B && (!x || !z || !eX || !eZ || !flags)))
         return fail(QEC_ERR_ARG, "qec_statistics_dev: bad argument");
     if (d->code->imp.empty()) return fail(QEC_ERR_UNSUPPORTED, "qec_statistics_dev: code has no I-P matrix");
-    QEC_HIP_CHECK(hipSetDevice(d->device));
+    int rc = single_device_only(d, "qec_statistics_dev");
+    if (rc) return rc;
+    QEC_DEVICE_SCOPE(d->device);
     return launch_statistics(*d->code, d->imp.data(), x, z, eX, eZ, flags, (long long)B,
                              reinterpret_cast<unsigned long long*>(counters), static_cast<hipStream_t>(stream));
 }
 
-int qec_monte_carlo(qec_decoder* d, uint64_t seed, uint64_t start, uint64_t count, float p, int maxIter, int stop,
-                    size_t batch, qec_mc_result* out)
+int qec_statistics_packed_dev(qec_decoder* d, const uint8_t* errp, const uint8_t* records, const int32_t* iters,
+                              size_t B, uint64_t* counters, void* stream)
 {
-    if (!d || !out || (stop < QEC_STOP_REF || stop > QEC_STOP_SYNDROME)) return fail(QEC_ERR_ARG, "qec_monte_carlo: bad argument");
-    const Code& c = *d->code;
-    if (c.imp.empty()) return fail(QEC_ERR_UNSUPPORTED, "qec_monte_carlo: code has no I-P matrix for the logical check");
-    QEC_HIP_CHECK(hipSetDevice(d->device));
-    if (batch == 0) batch = 65536;
-    const auto t0 = std::chrono::high_resolution_clock::now();
-    try {
-        mc_reserve(d, (size_t)std::min<uint64_t>(batch, std::max<uint64_t>(count, 1)), 0);
-    } catch (const std::exception& ex) {
-        return fail(QEC_ERR_HIP, std::string("qec_monte_carlo: ") + ex.what());
-    }
-    hipStream_t st = d->stream;
-    QEC_HIP_CHECK(hipMemsetAsync(d->mcount.data(), 0, QEC_MC_NCOUNTERS * sizeof(unsigned long long), st));
-    double dec_s = 0;
-    uint64_t itx = 0, itz = 0;
-    std::vector<int32_t> hit;
-    for (uint64_t base = 0; base < count; base += batch) {
-        const long long cnt = (long long)std::min<uint64_t>(batch, count - base);
-        int rc = launch_sample_depolarizing(seed, start + base, cnt, c.n, p, d->mx.data(), d->mz.data(), st);
-        if (rc) return rc;
-        rc = mc_decode_and_count(d, cnt, p, maxIter, stop, dec_s);
-        if (rc) return rc;
-        hit.resize(2 * (size_t)cnt);
-        QEC_HIP_CHECK(hipMemcpyAsync(hit.data(), d->mit.data(), hit.size() * sizeof(int32_t), hipMemcpyDeviceToHost, st));
-        QEC_HIP_CHECK(hipStreamSynchronize(st));
-        for (long long k = 0; k < cnt; ++k) { itx += hit[2 * k]; itz += hit[2 * k + 1]; }
-    }
-    unsigned long long cn[QEC_MC_NCOUNTERS];
-    QEC_HIP_CHECK(hipMemcpyAsync(cn, d->mcount.data(), sizeof cn, hipMemcpyDeviceToHost, st));
-    QEC_HIP_CHECK(hipStreamSynchronize(st));
-    const auto t1 = std::chrono::high_resolution_clock::now();
-    out->tested = count;
-    out->withX = cn[QEC_MC_WITHX]; out->withZ = cn[QEC_MC_WITHZ];
-    out->synX = cn[QEC_MC_SYNX]; out->synZ = cn[QEC_MC_SYNZ];
-    out->logical = cn[QEC_MC_LOGICAL]; out->corrected = cn[QEC_MC_CORRECTED];
-    out->convX = cn[QEC_MC_CONVX]; out->convZ = cn[QEC_MC_CONVZ];
-    out->iterationsX = itx; out->iterationsZ = itz;
-    out->decodeSeconds = dec_s;
-    out->totalSeconds = std::chrono::duration<double>(t1 - t0).count();
-    return QEC_OK;
+    if (!d || !counters || (B && (!errp || !records))) return fail(QEC_ERR_ARG, "qec_statistics_packed_dev: bad argument");
+    if (d->code->imp.empty()) return fail(QEC_ERR_UNSUPPORTED, "qec_statistics_packed_dev: code has no I-P matrix");
+    int rc = single_device_only(d, "qec_statistics_packed_dev");
+    if (rc) return rc;
+    QEC_DEVICE_SCOPE(d->device);
+    return launch_statistics_packed(*d->code, d->imp_rec.data(), errp, records, iters, (long long)B,
+                                    reinterpret_cast<unsigned long long*>(counters), static_cast<hipStream_t>(stream));
 }
 
 }  // extern "C"

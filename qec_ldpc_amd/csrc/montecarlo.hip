@@ -6,8 +6,9 @@
 //     reference's fixed-weight draws (host mt19937 stream, DecoderCPU.h:448-459)
 //     expanded on the device;
 //   * syndromes: s(r, i) = XOR_l e[l P + (E[r][l] + i) mod P]  (GetSyndromeX/Z,
-//     Quantum_LDPC_Code.h:94-124, through the circulant tables);
-//   * statistics: residual e ^ e_hat bit-packed with ballots, I-P logical check
+//     Quantum_LDPC_Code.h:94-124, through the circulant tables), fused with the errors
+//     (mc_errors_syndrome_kernel: one wave per sample, errors staged in LDS);
+//   * statistics: residual e ^ e_hat bit-packed, I-P logical check
 //     (Quantum_LDPC_Code.h:126-142) on bit-packed rows, and the CodeStatistics
 //     counters (DecoderCPU.h:464-521) reduced per block.
 // These are integer/byte kernels: HBM/L2-bound, not worth MFMA.
@@ -15,6 +16,7 @@
 
 #include <cstdint>
 
+#include "qec_device.h"
 #include "qec_internal.h"
 
 namespace qec {
@@ -57,71 +59,6 @@ __global__ void sample_depolarizing_kernel(uint64_t seed, uint64_t start, long l
     const uint32_t type = (uint32_t)(((uint64_t)o.y * 3u) >> 32);
     x[t] = (uint8_t)(hit && type != 2);
     z[t] = (uint8_t)(hit && type != 0);
-}
-
-// Reference fixed-weight draws (index, type) -> dense errors (x, z pre-zeroed).
-__global__ void errors_from_draws_kernel(const int32_t* __restrict__ idx, const uint8_t* __restrict__ type,
-                                         long long B, int W, int n, uint8_t* __restrict__ x, uint8_t* __restrict__ z)
-{
-    const long long b = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (b >= B) return;
-    for (int w = 0; w < W; ++w) {
-        const int v = idx[b * W + w];
-        const int t = type[b * W + w];
-        if (t == 0 || t == 1) x[b * n + v] = 1;  // DecoderCPU.h:456-457
-        if (t == 2 || t == 1) z[b * n + v] = 1;
-    }
-}
-
-struct SynArgs {
-    const uint8_t* x;
-    const uint8_t* z;
-    uint8_t* sX;
-    uint8_t* sZ;
-    long long B;
-    int n, L, P, mX, mZ;
-    int EX[128], EZ[128];
-};
-
-// one thread per (sample, check) over both sectors
-__global__ void syndrome_kernel(const SynArgs a)
-{
-    const int m = a.mX + a.mZ;
-    const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= a.B * m) return;
-    const long long b = t / m;
-    int c = (int)(t - b * m);
-    const bool zs = c >= a.mX;
-    if (zs) c -= a.mX;
-    const int r = c / a.P, i = c - r * a.P;
-    const int* E = zs ? a.EZ : a.EX;
-    const uint8_t* e = (zs ? a.z : a.x) + b * a.n;
-    uint32_t s = 0;
-    for (int l = 0; l < a.L; ++l) {
-        int j = E[r * a.L + l] + i;
-        j -= (j >= a.P) ? a.P : 0;
-        s ^= e[l * a.P + j] & 1u;
-    }
-    (zs ? a.sZ : a.sX)[b * (zs ? a.mZ : a.mX) + c] = (uint8_t)s;
-}
-
-// Any regular code (sparse-graph engine): s(c) = XOR_k e[chkVar[c dc + k]], the check's
-// variables from the engine's InitIndexArrays table; one thread per (sample, check).
-__global__ void syndrome_csr_kernel(const uint8_t* __restrict__ x, const uint8_t* __restrict__ z,
-                                    const int32_t* __restrict__ chkVar, long long B, int n, int mX, int mZ, int dc,
-                                    uint8_t* __restrict__ sX, uint8_t* __restrict__ sZ)
-{
-    const int m = mX + mZ;
-    const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= B * m) return;
-    const long long b = t / m;
-    const int c = (int)(t - b * m);
-    const bool zs = c >= mX;
-    const uint8_t* e = (zs ? z : x) + b * n;
-    const int32_t* vars = chkVar + (size_t)c * dc;
-    uint32_t s = 0;
-    for (int k = 0; k < dc; ++k) s ^= e[vars[k]] & 1u;
-    if (zs) sZ[b * mZ + (c - mX)] = (uint8_t)s; else sX[b * mX + c] = (uint8_t)s;
 }
 
 // counters, in qec_mc_counters order
@@ -216,6 +153,172 @@ __global__ void pack_decisions_kernel(const uint8_t* __restrict__ eX, const uint
     out[t] = (uint8_t)v;
 }
 
+// ---- fused Monte-Carlo front end ----------------------------------------------------
+// One wave per sample, errors staged in LDS (this wave's x and z rows, each zero-padded to
+// npad = 8 nb bytes):
+//   source PHILOX: the depolarising sampler above, qubit by qubit (nothing read from HBM);
+//   source DRAWS:  the reference's W (index, type) draws of the sample (DecoderCPU.h:452-457);
+//   source BYTES:  x, z rows [B][n] from HBM.
+// Then, from LDS: the syndromes sX, sZ (QC: s(r, i) = XOR_l e[l P + (E[r][l] + i) mod P]; any other
+// regular code: the check's variables from the sparse engine's table), and the bit-packed errors
+// errp [B][2 nb] in the decision-record layout (x bits, then z bits) for the statistics kernel.
+// HBM traffic per P61 sample: 549 B of syndromes + 154 B of packed errors written.
+constexpr int kMcWaves = 4;
+
+struct McArgs {
+    // sources
+    uint64_t seed, start, thr;                 // PHILOX
+    const int32_t* idx;                        // DRAWS: [B][W] qubit indices
+    const uint8_t* type;                       //        [B][W] 0 = X, 1 = Y, 2 = Z
+    int W;
+    const uint8_t* x;                          // BYTES: [B][n]
+    const uint8_t* z;
+    // outputs
+    uint8_t* sX;                               // [B][mX]
+    uint8_t* sZ;                               // [B][mZ]
+    uint8_t* errp;                             // [B][2 nb] (nullable)
+    const int32_t* chkVar;                     // non-QC codes: [(mX + mZ) L] variables per check
+    long long B;
+    int n, nb, L, P, mX, mZ;
+    int EX[128], EZ[128];
+};
+
+template <int SRC>
+__global__ __launch_bounds__(64 * kMcWaves) void mc_errors_syndrome_kernel(const McArgs a)
+{
+    extern __shared__ __attribute__((aligned(8))) uint8_t mc_smem[];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const long long b = (long long)blockIdx.x * kMcWaves + wv;
+    if (b >= a.B) return;  // wave-local from here on: no workgroup barrier
+    const int n = a.n, npad = 8 * a.nb;
+    uint8_t* __restrict__ ex = mc_smem + (size_t)wv * 2 * npad;
+    uint8_t* __restrict__ ez = ex + npad;
+    if constexpr (SRC == MC_SRC_DRAWS) {
+        for (int v = lane; v < npad; v += 64) { ex[v] = 0; ez[v] = 0; }
+        wave_sync();
+        for (int w = lane; w < a.W; w += 64) {
+            const int v = a.idx[b * a.W + w];
+            const int t = a.type[b * a.W + w];
+            if (t == 0 || t == 1) ex[v] = 1;  // several draws may hit one qubit: they all store 1
+            if (t == 2 || t == 1) ez[v] = 1;
+        }
+    } else {
+        for (int v = lane; v < npad; v += 64) {
+            uint8_t xv = 0, zv = 0;
+            if (v < n) {
+                if constexpr (SRC == MC_SRC_PHILOX) {
+                    const uint64_t sb = a.start + (uint64_t)b;
+                    const U4 o = philox4x32_10(U4{(uint32_t)sb, (uint32_t)(sb >> 32), (uint32_t)v, kPhiloxSalt},
+                                               (uint32_t)a.seed, (uint32_t)(a.seed >> 32));
+                    const bool hit = (uint64_t)o.x < a.thr;
+                    const uint32_t type = (uint32_t)(((uint64_t)o.y * 3u) >> 32);
+                    xv = (uint8_t)(hit && type != 2);
+                    zv = (uint8_t)(hit && type != 0);
+                } else {
+                    xv = a.x[b * n + v] & 1u;
+                    zv = a.z[b * n + v] & 1u;
+                }
+            }
+            ex[v] = xv;
+            ez[v] = zv;
+        }
+    }
+    wave_sync();
+    const int m = a.mX + a.mZ;
+    for (int c = lane; c < m; c += 64) {
+        const bool zs = c >= a.mX;
+        const int cc = zs ? c - a.mX : c;
+        const uint8_t* e = zs ? ez : ex;
+        uint32_t s = 0;
+        if (a.chkVar != nullptr) {
+            const int32_t* vars = a.chkVar + (size_t)c * a.L;
+            for (int k = 0; k < a.L; ++k) s ^= e[vars[k]];
+        } else {
+            const int r = cc / a.P, i = cc - r * a.P;
+            const int* E = zs ? a.EZ : a.EX;
+            for (int l = 0; l < a.L; ++l) {
+                int j = E[r * a.L + l] + i;
+                j -= (j >= a.P) ? a.P : 0;
+                s ^= e[l * a.P + j];
+            }
+        }
+        (zs ? a.sZ + b * a.mZ : a.sX + b * a.mX)[cc] = (uint8_t)(s & 1u);
+    }
+    if (a.errp != nullptr) {
+        for (int t = lane; t < 2 * a.nb; t += 64) {
+            const int k = t < a.nb ? t : t - a.nb;
+            const uint8_t* e = t < a.nb ? ex : ez;
+            a.errp[b * 2 * a.nb + t] = (uint8_t)pack8(*reinterpret_cast<const uint64_t*>(e + 8 * k));
+        }
+    }
+}
+
+// CodeStatistics counters of a batch from bit-packed errors errp [B][2 nb] and decision records
+// rec [B][2 nb + 1] (qec_decode_batch_packed_dev): the residual [x ^ eX | z ^ eZ] is their XOR
+// over the first 2 nb bytes, tested against the I-P rows packed in the same layout
+// (Code::imp_rows_rec); optional iteration sums (iters [B][2]) into counters[8], counters[9].
+// One wave per sample; counters as statistics_kernel (DecoderCPU.h:464-521).
+constexpr int kMaxRecWords = 80;  // 2 nb <= 640 bytes
+
+__global__ __launch_bounds__(64 * kStatWaves) void statistics_packed_kernel(
+    const uint8_t* __restrict__ errp, const uint8_t* __restrict__ rec, const int32_t* __restrict__ iters, long long B,
+    int nb, const uint64_t* __restrict__ imp_rows, int imp_nrows, int imp_words, unsigned long long* __restrict__ counters)
+{
+    __shared__ unsigned long long part[C_N + 2];
+    __shared__ __attribute__((aligned(8))) uint8_t sres[kStatWaves][8 * kMaxRecWords];
+    if (threadIdx.x < C_N + 2) part[threadIdx.x] = 0;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const long long b = (long long)blockIdx.x * kStatWaves + wv;
+    const bool live = b < B;
+    const int recB = 2 * nb + 1;
+    bool anyX = false, anyZ = false;
+    if (live) {
+        for (int t = lane; t < 8 * imp_words; t += 64) {
+            uint8_t r = 0;
+            if (t < 2 * nb) {
+                const uint8_t e = errp[b * 2 * nb + t];
+                if (t < nb) anyX |= e != 0; else anyZ |= e != 0;
+                r = e ^ rec[b * recB + t];
+            }
+            sres[wv][t] = r;
+        }
+    }
+    __syncthreads();
+    if (live) {
+        const uint8_t f = rec[b * recB + 2 * nb];
+        const bool wx = __any(anyX), wz = __any(anyZ);
+        const bool dEX = f & QEC_SYNDROME_FAIL_X, dEZ = f & QEC_SYNDROME_FAIL_Z;
+        bool logical = false;
+        if (!(dEX || dEZ) && imp_nrows > 0) {  // CheckLogicalError only when no syndrome failure
+            const uint64_t* res = reinterpret_cast<const uint64_t*>(sres[wv]);
+            bool odd = false;
+            for (int row = lane; row < imp_nrows; row += 64) {
+                const uint64_t* rp = imp_rows + (size_t)row * imp_words;
+                unsigned long long acc = 0;
+                for (int w = 0; w < imp_words; ++w) acc ^= rp[w] & res[w];
+                odd |= (__popcll(acc) & 1) != 0;
+            }
+            logical = __any(odd);
+        }
+        if (lane == 0) {
+            atomicAdd(&part[C_WITHX], (unsigned long long)wx);
+            atomicAdd(&part[C_WITHZ], (unsigned long long)wz);
+            atomicAdd(&part[C_SYNX], (unsigned long long)dEX);
+            atomicAdd(&part[C_SYNZ], (unsigned long long)dEZ);
+            if (!(dEX || dEZ)) atomicAdd(&part[logical ? C_LOGICAL : C_CORRECTED], 1ull);
+            atomicAdd(&part[C_CONVX], (unsigned long long)((f & QEC_CONVERGENCE_FAIL_X) != 0));
+            atomicAdd(&part[C_CONVZ], (unsigned long long)((f & QEC_CONVERGENCE_FAIL_Z) != 0));
+            if (iters != nullptr) {
+                atomicAdd(&part[C_N], (unsigned long long)iters[2 * b]);
+                atomicAdd(&part[C_N + 1], (unsigned long long)iters[2 * b + 1]);
+            }
+        }
+    }
+    __syncthreads();
+    const int nc = iters != nullptr ? C_N + 2 : C_N;
+    if (threadIdx.x < nc && part[threadIdx.x]) atomicAdd(&counters[threadIdx.x], part[threadIdx.x]);
+}
+
 // ---- launchers --------------------------------------------------------------
 static int launch_check(const char* what)
 {
@@ -236,37 +339,46 @@ int launch_sample_depolarizing(uint64_t seed, uint64_t start, long long B, int n
     return launch_check("sample_depolarizing");
 }
 
-int launch_errors_from_draws(const int32_t* idx, const uint8_t* type, long long B, int W, int n, uint8_t* x,
-                             uint8_t* z, hipStream_t st)
+int launch_mc_errors_syndrome(int src, const McArgsHost& h, hipStream_t st)
 {
-    if (B <= 0) return QEC_OK;
-    if (hipMemsetAsync(x, 0, (size_t)B * n, st) != hipSuccess || hipMemsetAsync(z, 0, (size_t)B * n, st) != hipSuccess)
-        return fail(QEC_ERR_HIP, "errors_from_draws: memset");
-    if (W > 0)
-        hipLaunchKernelGGL(errors_from_draws_kernel, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, st, idx, type, B,
-                           W, n, x, z);
-    return launch_check("errors_from_draws");
+    if (h.B <= 0) return QEC_OK;
+    const Code& c = *h.code;
+    McArgs a{};
+    a.seed = h.seed; a.start = h.start;
+    const double pd = h.p;
+    a.thr = pd <= 0.0 ? 0ull : pd >= 1.0 ? (1ull << 32) : (uint64_t)(pd * 4294967296.0);
+    a.idx = h.idx; a.type = h.type; a.W = h.W;
+    a.x = h.x; a.z = h.z;
+    a.sX = h.sX; a.sZ = h.sZ; a.errp = h.errp;
+    a.chkVar = h.chkVar;
+    a.B = h.B;
+    a.n = c.n; a.nb = (c.n + 7) / 8; a.L = c.L; a.P = c.P; a.mX = c.mX; a.mZ = c.mZ;
+    if (a.chkVar == nullptr) {
+        if (!c.is_qc || c.J * c.L > 128 || c.K * c.L > 128) return fail(QEC_ERR_UNSUPPORTED, "mc front end: needs a QC code or a check table");
+        for (size_t k = 0; k < c.EX.size(); ++k) a.EX[k] = c.EX[k];
+        for (size_t k = 0; k < c.EZ.size(); ++k) a.EZ[k] = c.EZ[k];
+    }
+    const size_t smem = (size_t)kMcWaves * 2 * 8 * a.nb;
+    if (smem > 64 * 1024) return fail(QEC_ERR_UNSUPPORTED, "mc front end: code too long for the LDS stage");
+    const dim3 grid((unsigned)((h.B + kMcWaves - 1) / kMcWaves)), block(64 * kMcWaves);
+    if (src == MC_SRC_PHILOX)
+        hipLaunchKernelGGL(mc_errors_syndrome_kernel<MC_SRC_PHILOX>, grid, block, smem, st, a);
+    else if (src == MC_SRC_DRAWS)
+        hipLaunchKernelGGL(mc_errors_syndrome_kernel<MC_SRC_DRAWS>, grid, block, smem, st, a);
+    else
+        hipLaunchKernelGGL(mc_errors_syndrome_kernel<MC_SRC_BYTES>, grid, block, smem, st, a);
+    return launch_check("mc_errors_syndrome");
 }
 
-int launch_syndrome(const Code& c, const int32_t* chkVar, const uint8_t* x, const uint8_t* z, long long B,
-                    uint8_t* sX, uint8_t* sZ, hipStream_t st)
+int launch_statistics_packed(const Code& c, const uint64_t* imp_rec_dev, const uint8_t* errp, const uint8_t* rec,
+                             const int32_t* iters, long long B, unsigned long long* counters, hipStream_t st)
 {
     if (B <= 0) return QEC_OK;
-    if (chkVar != nullptr) {
-        const long long tot = B * (c.mX + c.mZ);
-        hipLaunchKernelGGL(syndrome_csr_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, x, z, chkVar, B,
-                           c.n, c.mX, c.mZ, c.L, sX, sZ);
-        return launch_check("syndrome_csr");
-    }
-    if (!c.is_qc || c.J * c.L > 128 || c.K * c.L > 128) return fail(QEC_ERR_UNSUPPORTED, "syndrome kernel: needs a QC code");
-    SynArgs a{};
-    a.x = x; a.z = z; a.sX = sX; a.sZ = sZ; a.B = B;
-    a.n = c.n; a.L = c.L; a.P = c.P; a.mX = c.mX; a.mZ = c.mZ;
-    for (size_t k = 0; k < c.EX.size(); ++k) a.EX[k] = c.EX[k];
-    for (size_t k = 0; k < c.EZ.size(); ++k) a.EZ[k] = c.EZ[k];
-    const long long tot = B * (c.mX + c.mZ);
-    hipLaunchKernelGGL(syndrome_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, a);
-    return launch_check("syndrome");
+    if (c.imp_words_rec > kMaxRecWords) return fail(QEC_ERR_UNSUPPORTED, "packed statistics kernel: 2 ceil(n/8) > 640");
+    const int nrows = c.imp_words_rec ? (int)(c.imp_rows_rec.size() / c.imp_words_rec) : 0;
+    hipLaunchKernelGGL(statistics_packed_kernel, dim3((unsigned)((B + kStatWaves - 1) / kStatWaves)), dim3(64 * kStatWaves),
+                       0, st, errp, rec, iters, B, (c.n + 7) / 8, imp_rec_dev, nrows, c.imp_words_rec, counters);
+    return launch_check("statistics_packed");
 }
 
 int launch_statistics(const Code& c, const uint64_t* imp_dev, const uint8_t* x, const uint8_t* z, const uint8_t* eX,

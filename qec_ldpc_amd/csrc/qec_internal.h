@@ -10,7 +10,7 @@
 namespace qec {
 
 // BpArgs::hardPaths bits (from QEC_OPT_HARD_PATHS / QEC_OPT_CYCLE_JUMP)
-enum { QEC_HP_FORMS = 1, QEC_HP_CYCLE = 2 };
+enum { QEC_HP_FORMS = 1, QEC_HP_CYCLE = 2, QEC_HP_PHASE = 4 /* launch the instrumented kernel */ };
 
 // Thread-local last-error text behind qec_last_error().
 void set_error(const std::string& msg);
@@ -29,6 +29,10 @@ struct Code {
     // Bit-packed I-P rows that are not all-zero (for CheckLogicalError).
     int imp_words = 0;                 // u64 words per packed 2n-bit row
     std::vector<uint64_t> imp_rows;    // nnz_rows x imp_words
+    // The same rows in the decision-record layout (qec_decode_batch_packed_dev): x qubit q at bit q,
+    // z qubit t at bit 8 ceil(n/8) + t.
+    int imp_words_rec = 0;
+    std::vector<uint64_t> imp_rows_rec;
     std::string describe() const;      // operator<< of Quantum_LDPC_Code.h:145-150
 };
 
@@ -51,6 +55,25 @@ struct Mt19937 {
     explicit Mt19937(uint32_t seed);
     uint32_t next();
     uint32_t msvc_uniform(uint32_t N);  // uniform_int_distribution<int>(0, N-1)
+};
+
+// Host description of a fused Monte-Carlo front-end launch (montecarlo.hip,
+// mc_errors_syndrome_kernel): error source (MC_SRC_*), syndromes out, packed errors out.
+enum { MC_SRC_PHILOX = 0, MC_SRC_DRAWS = 1, MC_SRC_BYTES = 2 };
+struct McArgsHost {
+    const Code* code = nullptr;
+    uint64_t seed = 0, start = 0;
+    float p = 0.0f;                 // PHILOX
+    const int32_t* idx = nullptr;   // DRAWS
+    const uint8_t* type = nullptr;
+    int W = 0;
+    const uint8_t* x = nullptr;     // BYTES
+    const uint8_t* z = nullptr;
+    uint8_t* sX = nullptr;
+    uint8_t* sZ = nullptr;
+    uint8_t* errp = nullptr;        // [B][2 ceil(n/8)], nullable
+    const int32_t* chkVar = nullptr;
+    long long B = 0;
 };
 
 }  // namespace qec

@@ -84,7 +84,7 @@ __global__ __launch_bounds__(kHistThreads) void schedule_hist_kernel(const uint8
                                                                    int mX, int mZ, int chunk,
                                                                    uint8_t* __restrict__ key,
                                                                    uint32_t* __restrict__ counts,
-                                                                   uint8_t* __restrict__ zero_flags)
+                                                                   uint32_t* __restrict__ zero_merge)
 {
     __shared__ uint32_t h[kBuckets];
     const int t = threadIdx.x;
@@ -106,7 +106,7 @@ __global__ __launch_bounds__(kHistThreads) void schedule_hist_kernel(const uint8
             const int bk = kBuckets - 1 - (int)(w < kBuckets - 1 ? w : kBuckets - 1);
             key[b] = (uint8_t)bk;
             atomicAdd(&h[bk], 1u);
-            if (zero_flags) zero_flags[b] = 0;  // sector-split launches OR their flags in
+            if (zero_merge) zero_merge[b] = 0u;  // sector-split launches merge their flags there
         }
     }
     __syncthreads();
@@ -192,10 +192,10 @@ size_t schedule_workspace_bytes(long long B, int, int)
 }
 
 // Fills the workspace (schedule_workspace_bytes bytes) and returns in *perm_out the
-// heaviest-first order of the batch.  zero_flags (nullable): B bytes the hist pass zeroes on
-// the way (the sector-split decode ORs its flags into them).
+// heaviest-first order of the batch.  zero_merge (nullable): B words the hist pass zeroes on
+// the way (the sector-split decode merges its two sectors' flags there, bp_decode.hip).
 int launch_schedule(const uint8_t* sX, const uint8_t* sZ, long long B, int mX, int mZ, void* ws,
-                    uint8_t* zero_flags, int32_t** perm_out, hipStream_t st)
+                    uint32_t* zero_merge, int32_t** perm_out, hipStream_t st)
 {
     if (B > schedule_max_batch()) return fail(QEC_ERR_ARG, "schedule: batch too large to order");
     const bool shortrows = mX + mZ <= kShortRows;
@@ -208,10 +208,10 @@ int launch_schedule(const uint8_t* sX, const uint8_t* sZ, long long B, int mX, i
     *perm_out = perm;
     if (shortrows)
         hipLaunchKernelGGL(schedule_hist_kernel<1>, dim3(nch), dim3(kHistThreads), 0, st, sX, sZ, B, mX, mZ, chunk, key,
-                           counts, zero_flags);
+                           counts, zero_merge);
     else
         hipLaunchKernelGGL(schedule_hist_kernel<kHistSplitLong>, dim3(nch), dim3(kHistThreads), 0, st, sX, sZ, B, mX, mZ,
-                           chunk, key, counts, zero_flags);
+                           chunk, key, counts, zero_merge);
     hipLaunchKernelGGL(schedule_scatter_kernel, dim3(nch), dim3(kScatThreads), 0, st, key, B, chunk, nch, counts,
                        perm);
     const hipError_t err = hipGetLastError();

@@ -34,7 +34,7 @@ def test_exports_are_c_linkage():
 
 
 def test_abi_version_and_error_text():
-    assert q.lib().qec_abi_version() == 3
+    assert q.lib().qec_abi_version() == 4
     assert q.lib().qec_code_load(b"/nonexistent/code.txt") is None
     assert "Unable to find code file" in q.last_error()
 

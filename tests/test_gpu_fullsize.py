@@ -103,3 +103,60 @@ def test_schedule_split_off_identical(run):
         dec.set_option("sector_split", 1)
     for a, b in zip(run["out"][:4], off[:4]):
         assert np.array_equal(a, b)
+
+
+# ---- BASELINE configs[3]: 2^20 P61 syndromes @ 50 fixed iterations ---------------------------
+@pytest.fixture(scope="module")
+def mega(code_paths):
+    """The whole configs[3] batch decoded on one GPU in one packed launch, plus its syndromes."""
+    import torch
+    code = q.Quantum_LDPC_Code.createFromFile(code_paths["P61"])
+    B = 1 << 20
+    dec = q.DecoderGPU(code, 0, max_batch=B)
+    dev = torch.device("cuda", 0)
+    sX = torch.empty((B, code.numEqsX), dtype=torch.uint8, device=dev)
+    sZ = torch.empty((B, code.numEqsZ), dtype=torch.uint8, device=dev)
+    dec.sample_syndrome_dev(0x51EC0DE, 0, 0.01, sX, sZ)
+    rec = torch.empty((B, dec.record_bytes()), dtype=torch.uint8, device=dev)
+    dec.decode_batch_packed_dev(sX, sZ, 0.01, 50, "fixed", rec)
+    torch.cuda.synchronize()
+    return dict(code=code, dec=dec, B=B, sX=sX, sZ=sZ, rec=rec, path=code_paths["P61"])
+
+
+def test_configs3_oracle_subsample(mega):
+    rng = np.random.default_rng(2020)
+    idx = np.sort(rng.choice(mega["B"], 192, replace=False))
+    sX = mega["sX"].cpu().numpy()[idx]
+    sZ = mega["sZ"].cpu().numpy()[idx]
+    o = OracleCode(mega["path"]).decode_batch(sX, sZ, 0.01, 50, "fixed")
+    from qec_ldpc_amd.gather import pack_records
+    assert np.array_equal(mega["rec"].cpu().numpy()[idx], pack_records(o[0], o[1], o[2]))
+
+
+def test_configs3_shards_equal_single_launch(mega):
+    """configs[3]'s sharding: 8 contiguous shards decoded separately and gathered (concatenated in
+    rank order) give the single launch's records byte for byte."""
+    import torch
+    B, dec = mega["B"], mega["dec"]
+    parts = []
+    for g in range(8):
+        lo, hi = g * B // 8, (g + 1) * B // 8
+        r = torch.empty((hi - lo, dec.record_bytes()), dtype=torch.uint8, device=mega["rec"].device)
+        dec.decode_batch_packed_dev(mega["sX"][lo:hi], mega["sZ"][lo:hi], 0.01, 50, "fixed", r)
+        parts.append(r)
+    torch.cuda.synchronize()
+    assert torch.equal(torch.cat(parts), mega["rec"])
+
+
+def test_configs3_flags_consistent(mega):
+    """Flag bits against a recomputed H e on a 16 384-syndrome slice, and the batch decodes
+    (most low-p syndromes are satisfied)."""
+    from qec_ldpc_amd.gather import unpack_records
+    code = mega["code"]
+    sl = slice(500000, 500000 + 16384)
+    eX, eZ, fl = unpack_records(mega["rec"][sl].cpu().numpy(), code.n)
+    synx = (code.syndrome(0, eX) != mega["sX"][sl].cpu().numpy()).any(1)
+    synz = (code.syndrome(1, eZ) != mega["sZ"][sl].cpu().numpy()).any(1)
+    assert np.array_equal(synx, (fl & q.SYNDROME_FAIL_X) != 0)
+    assert np.array_equal(synz, (fl & q.SYNDROME_FAIL_Z) != 0)
+    assert synx.mean() < 0.01 and synz.mean() < 0.01

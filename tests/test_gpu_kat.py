@@ -1,7 +1,18 @@
-"""End-to-end known-answer tests on the GPU: DecoderGPU::GetStatistics (errors from
-the reference's mt19937(seed) stream, GPU decode with the reference stop rule,
-I-P logical check) reproduces the reference's published CodeStatistics counters,
-and the CLI (main.cu's loop) writes results blocks in the reference format."""
+"""End-to-end known-answer tests on the GPU: DecoderGPU::GetStatistics (errors from the
+reference's mt19937(seed) stream, GPU decode with the reference stop rule, I-P logical check)
+reproduces the reference's published CodeStatistics counters -- every block of
+QEC_LDPC/results/** (tests/golden/kat.json) -- and the CLI (main.cu's loop) writes results
+blocks in the reference format.
+
+The archived blocks (QEC_LDPC/results/archive/*) come from two generations of the reference
+(SURVEY.md section 4).  tests/golden/kat_archive.json, made by the ORACLE
+(tests/golden/classify_archive.py), says which counter mapping each follows:
+  full        every counter as published;
+  no_logical  written before logical-error detection existed: published Corrected =
+              Corrected + Logical of the current code, every other counter as published;
+  unmatched   neither (excluded here, with the reason in the skip message).
+"""
+import json
 import os
 import re
 import subprocess
@@ -9,13 +20,38 @@ import subprocess
 import pytest
 
 import qec_ldpc_amd as q
-from conftest import COUNTERS, code_key, kat_subset
+from conftest import COUNTERS, GOLDEN, ROOT, code_key
 
 pytestmark = pytest.mark.gpu
 
 MAP = {"tested": "numErrorsTested", "withX": "numXErrorsTested", "withZ": "numZErrorsTested",
        "corrected": "corrected", "synX": "syndromeErrorsX", "synZ": "syndromeErrorsZ",
        "logical": "logicalErrors", "convX": "convergenceFailX", "convZ": "convergenceFailZ"}
+
+
+def _records():
+    with open(os.path.join(GOLDEN, "kat.json")) as f:
+        recs = json.load(f)
+    cls = {}
+    path = os.path.join(GOLDEN, "kat_archive.json")
+    if os.path.exists(path):
+        with open(path) as f:
+            cls = {(r["set"], r["file"], r["block"]): r["class"] for r in json.load(f)}
+    out = []
+    for r in recs:
+        c = "full" if r["set"] not in ("archive", ".") else cls.get((r["set"], r["file"], r["block"]), "unclassified")
+        out.append((r, c))
+    return out
+
+
+RECORDS = _records()
+
+
+def _id(rc):
+    r, c = rc
+    m = re.search(r"_W_(\d+)_MAX_(\d+)_p_([0-9.]+)", r["file"])
+    return "%s-%s-W%s-MAX%s-p%s-b%d" % (r["set"].strip("[]").replace(",", "_")[:12], code_key(r), m.group(1),
+                                        m.group(2), m.group(3), r["block"])
 
 
 @pytest.fixture(scope="module")
@@ -27,20 +63,46 @@ def decoders(code_paths):
     return out
 
 
-@pytest.mark.parametrize("idx", range(10))
-def test_gpu_reproduces_published_counters(idx, kat_records, decoders):
-    rec = kat_subset(kat_records)[idx]
+@pytest.mark.parametrize("rc", RECORDS, ids=[_id(x) for x in RECORDS])
+def test_gpu_reproduces_published_counters(rc, decoders):
+    rec, cls = rc
+    if cls in ("unmatched", "unclassified"):
+        pytest.skip("archive block %s: the oracle (CPU restatement of the current DecoderCPU) reproduces it "
+                    "under neither known counter mapping" % cls)
     st = decoders[code_key(rec)].GetStatistics(rec["W"], rec["tested"], rec["p_run"], rec["MAX"], rec["seed"])
     got = {k: st[MAP[k]] for k in COUNTERS}
-    assert got == {k: rec[k] for k in COUNTERS}, (rec["file"], rec["block"])
+    if cls == "no_logical":
+        got["corrected"] += got["logical"]
+        got["logical"] = 0
+    assert got == {k: rec[k] for k in COUNTERS}, (rec["file"], rec["block"], cls)
     assert st["randSeed"] == rec["seed"] and st["errorWeight"] == rec["W"]
 
 
-def test_cli_drop_in(tmp_path, code_paths):
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+def test_every_archive_block_classified():
+    """The fixture classifies every archived block, and almost all of them reproduce."""
+    arch = [c for r, c in RECORDS if r["set"] in ("archive", ".")]
+    assert "unclassified" not in arch
+    assert arch.count("unmatched") <= 2
+
+
+def test_getstats_through_cpp_interface(code_paths, kat_records):
+    """DecoderGPU::GetStats (QEC_LDPC/DecoderGPU.h:193-228) on the flat error arrays of a
+    published block equals GetStatistics on its seed, on one device and on a two-part decoder."""
+    rec = [r for r in kat_records if r["set"] == "[2,3,6,7,2,3]" and r["file"].endswith("_W_5_MAX_100_p_0.02.txt")][0]
+    for devs in ("0", "0,0"):
+        r = subprocess.run([os.path.join(ROOT, "tools", "getstats_check"), code_paths["P7"], str(rec["W"]), "20000",
+                            str(rec["MAX"]), "0.02", str(rec["seed"]), "--devices", devs],
+                           capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stdout + r.stderr
+        out = json.loads(r.stdout.strip().splitlines()[-1])
+        assert out["getstats"] == out["getstatistics"] and out["getstats"][0] == 20000
+
+
+@pytest.mark.parametrize("flags", [[], ["--gpus", "1"], ["--devices", "0,0"]])
+def test_cli_drop_in(tmp_path, code_paths, flags):
     (tmp_path / "results").mkdir()
     (tmp_path / "init.txt").write_text("%s 1 2 2000 30 0.02\n" % code_paths["P7"])
-    r = subprocess.run([os.path.join(root, "tools", "qec_ldpc"), "init.txt"], cwd=tmp_path,
+    r = subprocess.run([os.path.join(ROOT, "tools", "qec_ldpc")] + flags + ["init.txt"], cwd=tmp_path,
                        capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr
     files = sorted(os.listdir(tmp_path / "results"))
@@ -51,3 +113,4 @@ def test_cli_drop_in(tmp_path, code_paths):
     assert fields["Code"] == "[J=3,K=3,L=6,P=7,s=2,t=3][[n=42,k=0]]"
     assert int(fields["Errors Tested"]) == 2000 and int(fields["Error Weight"]) == 2
     assert "Run complete." in (tmp_path / "output_log.txt").read_text()
+

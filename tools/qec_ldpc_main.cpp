@@ -4,6 +4,8 @@
 // main.cu:91-104) and the same output_log.txt journal (main.cu:45-52,114).
 // The only change vs main.cu is the engine: DecoderGPU instead of DecoderCPU.
 // Exit status is 0 on success (main.cu returns 1).
+// Optional flags before the init file: --gpus N (GPUs 0..N-1 of this node, one decoder
+// spanning them; counters are identical to one GPU) or --devices 0,3,5.
 #include <algorithm>
 #include <chrono>
 #include <ctime>
@@ -11,6 +13,7 @@
 #include <iostream>
 #include <sstream>
 #include <string>
+#include <vector>
 
 #include "DecoderGPU.h"
 #include "Quantum_LDPC_Code.h"
@@ -24,11 +27,27 @@ int main(int argc, char** argv)
     }
     std::time_t ts = std::chrono::system_clock::to_time_t(std::chrono::system_clock::now());
     log << std::endl << std::ctime(&ts);
-    if (argc != 2) {
+    std::vector<int> devices{0};
+    int a = 1;
+    for (; a + 1 < argc && std::string(argv[a]).rfind("--", 0) == 0; a += 2) {
+        const std::string flag = argv[a], val = argv[a + 1];
+        devices.clear();
+        if (flag == "--gpus") {
+            for (int k = 0; k < std::stoi(val); ++k) devices.push_back(k);
+        } else if (flag == "--devices") {
+            std::stringstream ss(val);
+            std::string tok;
+            while (std::getline(ss, tok, ',')) devices.push_back(std::stoi(tok));
+        } else {
+            std::cerr << "unknown flag " << flag << std::endl;
+            return 2;
+        }
+    }
+    if (argc - a != 1 || devices.empty()) {
         log << "Must provide initialization file." << std::endl;
         return 0;
     }
-    std::string initFile = argv[1];
+    std::string initFile = argv[a];
     std::ifstream init(initFile);
     if (!init.is_open()) {
         log << "Unable to open init file \"" << initFile
@@ -41,7 +60,7 @@ int main(int argc, char** argv)
     try {
         std::cout << "Creating code from file " << codeFile << std::endl;
         Quantum_LDPC_Code code = Quantum_LDPC_Code::createFromFile(codeFile);
-        DecoderGPU decoder(code);
+        DecoderGPU decoder(code, devices);
         std::cout << "Engine: " << decoder.Describe() << std::endl;
         int w, W, COUNT, MAX_ITERATIONS;
         float p;

@@ -55,8 +55,18 @@ tools/getstats_check: tools/getstats_check.cpp include/*.h $(LIB)
 oracle:
 	$(MAKE) -s -C oracle
 
+# Host-code race check under ThreadSanitizer: the product's code model and
+# the oracle (without OpenMP) driven from 8 threads over shared code objects; tests/test_tsan.py
+TSAN_BIN := build/tsan/tsan_check
+tsan: $(TSAN_BIN)
+$(TSAN_BIN): tests/tsan/tsan_check.cpp $(CSRC)/code_model.cpp oracle/qec_oracle.c $(CSRC)/qec_internal.h include/qec_ldpc.h
+	mkdir -p build/tsan
+	gcc -O1 -g -fsanitize=thread -ffp-contract=off -fPIC -c oracle/qec_oracle.c -o build/tsan/qec_oracle.o
+	g++ -O1 -g -std=c++17 -fsanitize=thread -c $(CSRC)/code_model.cpp -o build/tsan/code_model.o
+	g++ -O1 -g -std=c++17 -fsanitize=thread tests/tsan/tsan_check.cpp build/tsan/code_model.o build/tsan/qec_oracle.o -o $@ -lpthread
+
 clean:
 	rm -rf build $(LIB) tools/qec_ldpc tools/getstats_check
 	$(MAKE) -s -C oracle clean
 
-.PHONY: all oracle clean
+.PHONY: all oracle clean tsan

@@ -10,8 +10,9 @@ record: (code, W, MAX, p from the file name, seed, tested) -> the 8 counters.
 Only data is extracted; nothing from the reference's sources is kept.
 
 `p_run` is the errorProbability the block was actually produced with.  The P=61
-files whose names say p_0.01 reproduce only with 0.02, so
-their p_run is 0.02; everything else uses the file-name value.
+files of results/[4,5,10,61,9,49]/ whose names say p_0.01 reproduce only with 0.02
+(SURVEY.md section 4), so their p_run is 0.02; everything else, the top-level P=61
+p_0.01 file included (it reproduces with 0.01), uses the file-name value.
 """
 import json
 import os
@@ -69,7 +70,7 @@ def main():
             J, K, L, P, s, t, W, MAX = map(int, m.groups()[:8])
             p_file = float(m.group(9))
             code = "J_%d_K_%d_L_%d_P_%d_s_%d_t_%d" % (J, K, L, P, s, t)
-            p_run = 0.02 if (P == 61 and p_file == 0.01) else p_file
+            p_run = 0.02 if (sub == "[4,5,10,61,9,49]" and P == 61 and p_file == 0.01) else p_file
             with open(os.path.join(d, fn)) as f:
                 blocks = parse_blocks(f.read())
             for bi, b in enumerate(blocks):

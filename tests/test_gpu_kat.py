@@ -79,10 +79,9 @@ def test_gpu_reproduces_published_counters(rc, decoders):
 
 
 def test_every_archive_block_classified():
-    """The fixture classifies every archived block, and almost all of them reproduce."""
+    """The fixture classifies every archived block, and every one of them reproduces."""
     arch = [c for r, c in RECORDS if r["set"] in ("archive", ".")]
-    assert "unclassified" not in arch
-    assert arch.count("unmatched") <= 2
+    assert len(arch) == 89 and "unclassified" not in arch and "unmatched" not in arch
 
 
 def test_getstats_through_cpp_interface(code_paths, kat_records):

@@ -39,3 +39,29 @@ def test_oracle_p61_p001_label_needs_p002(kat_records, oracle_codes):
     st = oracle_codes["P61"].get_statistics(rec["W"], 2000, 0.01, rec["MAX"], rec["seed"])
     st2 = oracle_codes["P61"].get_statistics(rec["W"], 2000, 0.02, rec["MAX"], rec["seed"])
     assert st != st2
+
+
+def _archive(cls, k):
+    import json
+    import os
+    from conftest import GOLDEN
+    with open(os.path.join(GOLDEN, "kat_archive.json")) as f:
+        arch = {(r["set"], r["file"], r["block"]): r["class"] for r in json.load(f)}
+    with open(os.path.join(GOLDEN, "kat.json")) as f:
+        recs = [r for r in json.load(f) if r["set"] == "archive" and "_P_7_" in r["code"]
+                and arch[(r["set"], r["file"], r["block"])] == cls]
+    return recs[k]
+
+
+@pytest.mark.parametrize("cls,k", [("full", 0), ("full", 2), ("no_logical", 0), ("no_logical", 5)])
+def test_oracle_archive_mapping(cls, k, oracle_codes):
+    """The archive classification the GPU KAT test relies on (tests/golden/kat_archive.json,
+    made by classify_archive.py) holds for a sample of P7 archive blocks: "no_logical" blocks
+    were written before logical-error detection (published Corrected = Corrected + Logical)."""
+    rec = _archive(cls, k)
+    st = oracle_codes["P7"].get_statistics(rec["W"], rec["tested"], rec["p_run"], rec["MAX"], rec["seed"])
+    if cls == "no_logical":
+        assert st["logical"] > 0 and rec["logical"] == 0
+        st["corrected"] += st["logical"]
+        st["logical"] = 0
+    assert {k2: st[k2] for k2 in COUNTERS} == {k2: rec[k2] for k2 in COUNTERS}

@@ -1,14 +1,20 @@
-"""Reduce rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of `bench.py --no-cpu` into
-profiles/pmc_<code>.json, which bench.py reads for roofline.traffic.
+"""Reduce one tools/gpu/run_profile.sh directory (a rocprofv3 --kernel-trace --stats pass and
+the --pmc passes of `bench.py --no-extras`) into profiles/pmc_<code>.json, which bench.py
+reads for its VALU-issue roofline and `traffic`.
 
-HBM bytes per decode launch = 2 x FETCH_SIZE + WRITE_SIZE (both reported in KiB),
-following MI355X_MICROARCH.md 'HBM [CDNA4]': on gfx950 FETCH_SIZE counts half the
-bytes of a coalesced streaming read, WRITE_SIZE counts the bytes.  Only the BP
-decode kernel's dispatches are used (the sampler/syndrome kernels run before the
-timed region and are excluded).
+For the BP decode kernel (Kernel_Name contains bp_decode_kernel), per launch:
+  * HBM bytes = 2 x FETCH_SIZE + WRITE_SIZE (both reported in KiB), following
+    MI355X_MICROARCH.md 'HBM [CDNA4]': on gfx950 FETCH_SIZE counts half the bytes of a
+    coalesced streaming read, WRITE_SIZE counts the bytes;
+  * SQ_INSTS_VALU / _LDS / _SALU: wave instructions issued; SQ_WAVES; SQ_WAIT_ANY,
+    SQ_ACTIVE_INST_ANY, SQ_WAVE_CYCLES (quad-cycles), GRBM_GUI_ACTIVE (cycles);
+  * duration: the kernel-trace pass's average (the PMC passes serialise and slow kernels);
+  * VALU issue fraction = SQ_INSTS_VALU x 2 cycles / (1024 SIMDs x 2.4 GHz x duration).
+Per-syndrome values (÷ the launch's batch) let bench.py price other batch sizes of the same
+workload.
 
-Usage: python tools/gpu/pmc_summary.py --fetch DIR --write DIR --code p61
-       --batch 65536 --iters 50 --stop fixed --out profiles/pmc_p61.json
+Usage: python tools/gpu/pmc_summary.py --dir gpurun_out/prof_TAG/p61 --code p61
+       --bench gpurun_out/prof_TAG/p61/bench_trace.json --out profiles/pmc_p61.json
 """
 import argparse
 import csv
@@ -16,41 +22,83 @@ import glob
 import json
 import os
 
+KERNEL = "bp_decode_kernel"
 
-def counter_values(d, name, kernel_substr="bp_decode_kernel"):
-    vals, kname = [], None
+
+def counter_rows(d):
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         with open(f) as fh:
+            yield from csv.DictReader(fh)
+
+
+def per_dispatch(d, kernel=KERNEL):
+    """{counter: [value per dispatch]} and the kernel's metadata, decode kernel only."""
+    vals, meta = {}, {}
+    per = {}
+    for row in counter_rows(d):
+        if kernel not in row.get("Kernel_Name", ""):
+            continue
+        key = (row["Dispatch_Id"], row["Counter_Name"])
+        per[key] = per.get(key, 0.0) + float(row["Counter_Value"])
+        meta = {"kernel": row["Kernel_Name"], "vgpr": int(row["VGPR_Count"]), "sgpr": int(row["SGPR_Count"]),
+                "scratch_bytes_per_lane": int(row["Scratch_Size"]), "lds_bytes": int(row["LDS_Block_Size"]),
+                "workgroup": int(row["Workgroup_Size"])}
+    for (_, name), v in per.items():
+        vals.setdefault(name, []).append(v)
+    return vals, meta
+
+
+def trace_duration_ns(d, kernel=KERNEL):
+    durs = []
+    for f in glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True):
+        with open(f) as fh:
             for row in csv.DictReader(fh):
-                if row.get("Counter_Name") == name and kernel_substr in row.get("Kernel_Name", ""):
-                    vals.append(float(row["Counter_Value"]))
-                    kname = row["Kernel_Name"]
-    return vals, kname
+                if kernel in row.get("Kernel_Name", ""):
+                    durs.append(int(row["End_Timestamp"]) - int(row["Start_Timestamp"]))
+    return durs
 
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--fetch", required=True)
-    ap.add_argument("--write", required=True)
+    ap.add_argument("--dir", required=True)
     ap.add_argument("--code", required=True)
-    ap.add_argument("--batch", type=int, required=True)
-    ap.add_argument("--iters", type=int, required=True)
-    ap.add_argument("--stop", default="fixed")
+    ap.add_argument("--bench", required=True, help="bench.py JSON line of the trace pass (workload)")
     ap.add_argument("--out", required=True)
     a = ap.parse_args()
-    fv, kname = counter_values(a.fetch, "FETCH_SIZE")
-    wv, _ = counter_values(a.write, "WRITE_SIZE")
-    if not fv or not wv:
-        raise SystemExit("no FETCH_SIZE/WRITE_SIZE rows for the decode kernel under %s / %s" % (a.fetch, a.write))
-    fetch = sum(fv) / len(fv) * 1024.0
-    write = sum(wv) / len(wv) * 1024.0
-    out = {
-        "code": a.code, "batch": a.batch, "iters": a.iters, "stop": a.stop, "kernel": kname,
-        "dispatches": {"fetch": len(fv), "write": len(wv)},
-        "fetch_size_bytes_raw": round(fetch), "write_size_bytes": round(write),
-        "hbm_bytes_per_launch": round(2.0 * fetch + write),
-        "correction": "2 x FETCH_SIZE + WRITE_SIZE (MI355X_MICROARCH.md, HBM [CDNA4]: gfx950 FETCH_SIZE counts half)",
-    }
+    with open(a.bench) as f:
+        line = [x for x in f.read().splitlines() if x.startswith("{")][-1]
+    b = json.loads(line)
+    batch = b["config"]["per_gpu_batch"]
+    vals, meta = {}, {}
+    for sub in sorted(glob.glob(os.path.join(a.dir, "pmc*"))):
+        if os.path.isdir(sub):
+            v, m = per_dispatch(sub)
+            vals.update(v)
+            meta = meta or m
+    if "SQ_INSTS_VALU" not in vals:
+        raise SystemExit("no SQ_INSTS_VALU rows for the decode kernel under %s" % a.dir)
+    avg = {k: sum(v) / len(v) for k, v in vals.items()}
+    durs = trace_duration_ns(os.path.join(a.dir, "trace"))
+    dur_ns = sum(durs) / len(durs) if durs else None
+    out = {"code": a.code, "batch": batch, "iters": b["config"]["bp_iters"], "stop": b["config"]["stop"],
+           "p": b["config"]["p"], "output": b["config"].get("output"), **meta,
+           "dispatches": {k: len(v) for k, v in vals.items()},
+           "kernel_trace_avg_ns": dur_ns, "kernel_trace_dispatches": len(durs)}
+    per_launch = {k: round(v) for k, v in avg.items()}
+    out["per_launch"] = per_launch
+    if "FETCH_SIZE" in avg and "WRITE_SIZE" in avg:
+        hbm = 2.0 * avg["FETCH_SIZE"] * 1024.0 + avg["WRITE_SIZE"] * 1024.0
+        out["hbm_bytes_per_launch"] = round(hbm)
+        out["hbm_bytes_per_syndrome"] = hbm / batch
+        out["hbm_correction"] = "2 x FETCH_SIZE + WRITE_SIZE, KiB -> B (MI355X_MICROARCH.md, HBM [CDNA4])"
+    out["valu_insts_per_launch"] = round(avg["SQ_INSTS_VALU"])
+    out["valu_insts_per_syndrome"] = avg["SQ_INSTS_VALU"] / batch
+    if dur_ns:
+        issue_s = avg["SQ_INSTS_VALU"] * 2 / (1024 * 2.4e9)
+        out["valu_issue_frac"] = round(issue_s / (dur_ns * 1e-9), 4)
+        out["valu_issue_basis"] = "SQ_INSTS_VALU x 2 cycles / (1024 SIMDs x 2.4 GHz x kernel-trace duration)"
+    if "SQ_WAIT_ANY" in avg and "SQ_ACTIVE_INST_ANY" in avg:
+        out["wait_over_issue"] = round(avg["SQ_WAIT_ANY"] / max(avg["SQ_ACTIVE_INST_ANY"], 1), 4)
     with open(a.out, "w") as fh:
         json.dump(out, fh, indent=1)
     print(json.dumps(out))

@@ -116,6 +116,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--hard-paths", type=int, default=1, help="QEC_OPT_HARD_PATHS for the timed run")
+    ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
+                    help="decoder option for the timed run (qec_decoder_set_option), e.g. schedule=0")
     ap.add_argument("--no-gather", action="store_true", help="N > 1: skip the RCCL gather measurements")
     ap.add_argument("--no-extras", action="store_true",
                     help="only the timed steps (profiling runs: no full-arithmetic / phase / sustained re-timings)")
@@ -155,6 +157,9 @@ def main():
     B = hi - lo
     dec = q.DecoderGPU(code, local, max_batch=B)
     dec.set_option("hard_paths", args.hard_paths)
+    for kv in args.opt:
+        k, v = kv.split("=")
+        dec.set_option(k, int(v))
 
     # the rank's shard of the sample index space, drawn and turned into syndromes on the device
     # (fused Philox sampler + syndrome kernel) before the timed region
@@ -229,7 +234,8 @@ def main():
                 "syndromes resident in HBM",
         "config": {"workload": workload + ", " + stop_label, "code": code.describe(), "global_batch": global_batch,
                    "per_gpu_batch": B, "bp_iters": iters, "stop": args.stop, "p": p, "output": args.output,
-                   "parallelism": "dp%d" % world, "kernel": dec.describe()},
+                   "parallelism": "dp%d" % world, "kernel": dec.describe(),
+                   **({"options": args.opt} if args.opt else {})},
         "p": p,
         "mean_iterations": {"X": round(it_mean[0], 4), "Z": round(it_mean[1], 4)},
         "decode_ms": round(kernel_ms, 4),

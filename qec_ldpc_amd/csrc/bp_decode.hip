@@ -115,6 +115,10 @@ namespace qec {
 #ifndef QEC_ROW_HARD
 #define QEC_ROW_HARD 0
 #endif
+//   QEC_SYN_ROWBARRIER  the syndrome test of the syndrome stop rule rotates one row at a time
+#ifndef QEC_SYN_ROWBARRIER
+#define QEC_SYN_ROWBARRIER 1
+#endif
 #define QEC_PICK(macro, dflt) ((macro) >= 0 ? (macro) != 0 : (dflt))
 
 // Per-variant tuning: minimum waves per SIMD for the register allocator, and the options above.
@@ -311,6 +315,17 @@ __device__ __forceinline__ int select_lanes(int a, int b, unsigned long long m)
     return r;
 }
 
+// This lane's in-group index, recomputed from the lane id for compile-time P (so ln.i need not stay
+// live across a whole sector loop only for the outputs written after it; it spilled at 96 VGPRs).
+template <class SH>
+__device__ __forceinline__ int lane_i(const Lane& ln)
+{
+    if constexpr (SH::kStatic)
+        return (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)) % SH::kP;
+    else
+        return ln.i;
+}
+
 template <class SH>
 __device__ __forceinline__ int rot_addr(const Lane& ln, int s)
 {
@@ -340,6 +355,19 @@ __device__ __forceinline__ bool group_all(bool pred, int gb, int P)
     const unsigned long long bad = __ballot(!pred);
     const unsigned long long gm = (P >= 64 ? ~0ull : ((1ull << P) - 1ull)) << gb;
     return (bad & gm) == 0ull;
+}
+// The same for a shift provider: with compile-time P > 32 a wave holds one group (lanes
+// [0, P); the lanes above are never live), so the group mask is a constant rather than a
+// per-lane 64-bit value kept live across the whole kernel.
+template <class SH>
+__device__ __forceinline__ bool group_all_sh(bool pred, const Lane& ln, int P)
+{
+    if constexpr (SH::kStatic && 2 * SH::kP > 64) {
+        constexpr unsigned long long gm = SH::kP >= 64 ? ~0ull : ((1ull << SH::kP) - 1ull);
+        return (__ballot(!pred) & gm) == 0ull;
+    } else {
+        return group_all(pred, ln.gb, P);
+    }
 }
 
 __device__ __forceinline__ bool outside(float x) { return !(x > 0.01f && x < 0.99f); }
@@ -428,6 +456,9 @@ __device__ __forceinline__ void check_pass(float (&msg)[R][L], uint32_t sbits, u
 template <int R, int L>
 __device__ __forceinline__ void check_pass_hard(float (&msg)[R][L], uint32_t sbits)
 {
+    // laundered: the R row seeds below are recomputed at each use (2 VALU each) instead of being
+    // hoisted out of the iteration loop into R live registers (which spilled at 96 VGPRs)
+    asm volatile("" : "+v"(sbits));
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         uint32_t x = ((sbits >> r) & 1u) ? 0x3F800000u : 0u;
@@ -692,6 +723,11 @@ __device__ __forceinline__ bool lane_syndrome_ok(const BpArgs& a, uint32_t hdmas
             x ^= ((uint32_t)rot_i<SH>((int)hdmask, ln, sh == 0 ? 0 : P - sh) >> l) & 1u;
         }
         match &= (x == ((sbits >> r) & 1u));
+#if QEC_SYN_ROWBARRIER
+        // one row's L rotations in flight at a time: all R L at once (the scheduler's choice) held
+        // R L results live beside the sector's messages and spilled the syndrome-stop kernels
+        __builtin_amdgcn_sched_barrier(0);
+#endif
     }
     return match;
 }
@@ -730,9 +766,9 @@ __device__ __forceinline__ bool iteration(const BpArgs& a, float (&msg)[R][L], u
                                                        LAST || n >= QEC_TRACK_FROM);
     }
     if constexpr (STOP == QEC_STOP_REF) {
-        if (n % 10 == 0) return group_all(lane_converged<R, L>(msg), ln.gb, P);  // DecoderCPU.h:287-290
+        if (n % 10 == 0) return group_all_sh<SH>(lane_converged<R, L>(msg), ln, P);  // DecoderCPU.h:287-290
     } else if constexpr (STOP == QEC_STOP_SYNDROME) {
-        return group_all(lane_syndrome_ok<R, L, SEC, SH>(a, hdmask, sbits, ln), ln.gb, P);
+        return group_all_sh<SH>(lane_syndrome_ok<R, L, SEC, SH>(a, hdmask, sbits, ln), ln, P);
     }
     return false;
 }
@@ -800,9 +836,9 @@ __device__ __forceinline__ bool iteration0(const BpArgs& a, float (&msg)[R][L], 
         }
     }
     if constexpr (STOP == QEC_STOP_REF) {
-        return group_all(lane_converged<R, L>(msg), ln.gb, P);  // n = 0: DecoderCPU.h:287-290
+        return group_all_sh<SH>(lane_converged<R, L>(msg), ln, P);  // n = 0: DecoderCPU.h:287-290
     } else if constexpr (STOP == QEC_STOP_SYNDROME) {
-        return group_all(lane_syndrome_ok<R, L, SEC, SH>(a, hdmask, sbits, ln), ln.gb, P);
+        return group_all_sh<SH>(lane_syndrome_ok<R, L, SEC, SH>(a, hdmask, sbits, ln), ln, P);
     }
     return false;
 }
@@ -836,7 +872,7 @@ __device__ __forceinline__ int cycle_end(int n, int N)
 
 // Syndrome bits of this lane's checks (r, i), r = 0..R-1, as bit r.
 template <int R, int SEC, class SH>
-__device__ __forceinline__ uint32_t load_sbits(const BpArgs& a, const Lane& ln, long long b, bool in_range)
+__device__ __forceinline__ uint32_t load_sbits(const BpArgs& a, const Lane& ln, uint32_t b, bool in_range)
 {
     const int P = SH::P(a);
     const int m = R * P;
@@ -845,7 +881,7 @@ __device__ __forceinline__ uint32_t load_sbits(const BpArgs& a, const Lane& ln, 
     if (in_range) {
 #pragma unroll
         for (int r = 0; r < R; ++r)
-            sbits |= (uint32_t)(s[b * m + r * P + wrap(ln.i + SH::template rowoff<SEC>(a, r), P)] & 1) << r;
+            sbits |= (uint32_t)(s[(size_t)b * m + r * P + wrap(ln.i + SH::template rowoff<SEC>(a, r), P)] & 1) << r;
     }
     return sbits;
 }
@@ -868,11 +904,11 @@ constexpr int stage_bytes_per_wave()
 // eX / eZ bytes, or, for a packed launch, through the wave's LDS stage into the record's nb bytes of
 // this sector: lane i of a group packs bytes i, i + P, ... (8 staged bytes each, one 8-byte LDS read).
 template <int L, int SEC, class SH>
-__device__ __forceinline__ void emit_decisions(const BpArgs& a, const Lane& ln, long long b, bool in_range,
+__device__ __forceinline__ void emit_decisions(const BpArgs& a, const Lane& ln, uint32_t b, bool in_range,
                                                uint32_t hdmask, uint8_t* __restrict__ stage)
 {
     const int P = SH::P(a);
-    const int i = ln.i;
+    const int i = lane_i<SH>(ln);
     if (a.rec == nullptr) {
         uint8_t* __restrict__ e = SEC ? a.eZ : a.eX;
         if (in_range) {
@@ -883,7 +919,7 @@ __device__ __forceinline__ void emit_decisions(const BpArgs& a, const Lane& ln, 
         return;
     }
     const int nb = a.nb;
-    uint8_t* __restrict__ sg = stage + (ln.gb / P) * (nb * 8);
+    uint8_t* __restrict__ sg = (SH::kStatic && 2 * SH::kP > 64) ? stage : stage + (ln.gb / P) * (nb * 8);
     if (in_range) {
 #pragma unroll
         for (int l = 0; l < L; ++l) sg[l * P + wrap(i + SH::template coloff<SEC>(a, l), P)] = (uint8_t)((hdmask >> l) & 1u);
@@ -898,11 +934,11 @@ __device__ __forceinline__ void emit_decisions(const BpArgs& a, const Lane& ln, 
 }
 
 template <int R, int L, int SEC, int STOP, class SH, class TU>
-__device__ __forceinline__ void decode_sector(const BpArgs& a, Lane& ln, long long b, bool in_range, float pp,
+__device__ __forceinline__ void decode_sector(const BpArgs& a, Lane& ln, uint32_t b, bool in_range, float pp,
                                               uint32_t sbits, const float* __restrict__ tab0, uint32_t& flags,
                                               int& iters_out, uint8_t* __restrict__ stage)
 {
-    const int i = ln.i, gb = ln.gb;
+    const int i = ln.i;
     const int P = SH::P(a);
 
     // InitVarNodes: every edge starts at p' (DecoderCPU.h:135-148, 265-267)
@@ -974,6 +1010,7 @@ __device__ __forceinline__ void decode_sector(const BpArgs& a, Lane& ln, long lo
         return;
     }
     // ---- post-processing of Decode (DecoderCPU.h:354-384) ----
+    asm volatile("" : "+v"(sbits));  // its per-row bits are recomputed here, not held since the sector began
     const int* et = SH::template table<SEC>(a);
     bool conv, syn_ok;
     uint32_t hdmask = 0;  // e[v] of this lane's variables (l, (i + C[l]) mod P), bit l
@@ -995,9 +1032,9 @@ __device__ __forceinline__ void decode_sector(const BpArgs& a, Lane& ln, long lo
             match &= (x != 0u) == (((sbits >> r) & 1u) != 0u);
         }
         conv = true;
-        syn_ok = group_all(match, gb, P);
+        syn_ok = group_all_sh<SH>(match, ln, P);
     } else {
-        conv = group_all(lane_converged<R, L>(msg), gb, P);
+        conv = group_all_sh<SH>(lane_converged<R, L>(msg), ln, P);
 #pragma unroll
         for (int l = 0; l < L; ++l) {
             bool hd = false;  // e[v] = any edge message >= 0.5f (DecoderCPU.h:354-373)
@@ -1008,7 +1045,7 @@ __device__ __forceinline__ void decode_sector(const BpArgs& a, Lane& ln, long lo
             }
             hdmask |= (uint32_t)hd << l;
         }
-        syn_ok = group_all(lane_syndrome_ok<R, L, SEC, SH>(a, hdmask, sbits, ln), gb, P);
+        syn_ok = group_all_sh<SH>(lane_syndrome_ok<R, L, SEC, SH>(a, hdmask, sbits, ln), ln, P);
     }
     emit_decisions<L, SEC, SH>(a, ln, b, in_range, hdmask, stage);
 
@@ -1075,7 +1112,9 @@ void bp_decode_kernel(const BpArgs a)
     const long long slot = grp * G + g;
     const bool in_range = (g < G) && (slot < a.B);
     if (!__any(in_range)) return;
-    const long long b = (in_range && a.perm != nullptr) ? (long long)a.perm[slot] : slot;
+    // the syndrome index in 32 bits (launch_decode caps B below 2^31): a 64-bit index live across both
+    // sectors spilled at 96 VGPRs
+    const uint32_t b = (in_range && a.perm != nullptr) ? (uint32_t)a.perm[slot] : (uint32_t)slot;
 
     // p' = (2/3) p, as the reference writes it (DecoderCPU.h:259)
     const float pp = 2.0f / 3.0f * a.errorProbability;
@@ -1093,7 +1132,7 @@ void bp_decode_kernel(const BpArgs a)
     if (!QEC_PREFETCH_Z && (!doX || !SPLIT)) sbZ = load_sbits<RZ, 1, SH>(a, ln, b, in_range);
     if (!doX || !SPLIT)
         decode_sector<RZ, L, 1, STOP, SH, TU>(a, ln, b, in_range, pp, sbZ, tab0 + kTabX, flags, itZ, stage);
-    if (in_range && i == 0) {
+    if (in_range && lane_i<SH>(ln) == 0) {
         uint8_t* fdst = a.rec != nullptr ? a.rec + b * (long long)a.recBytes + 2 * a.nb : a.flags + b;
         if constexpr (!SPLIT) {
             *fdst = (uint8_t)flags;
@@ -1311,6 +1350,7 @@ int launch_decode(const void* variant, const Code& c, const uint8_t* sX, const u
 {
     const Variant* v = static_cast<const Variant*>(variant);
     if (B <= 0) return QEC_OK;
+    if (B >= (1LL << 31)) return fail(QEC_ERR_ARG, "bp_decode: at most 2^31 - 1 syndromes per launch");
     BpArgs a{};
     a.sX = sX; a.sZ = sZ; a.eX = eX; a.eZ = eZ; a.flags = flags; a.iters = iters; a.q = q;
     a.rec = rec;

@@ -15,16 +15,15 @@
 // index).  The order inside one (chunk, bucket) depends on LDS-atomic timing and is not
 // deterministic, which is harmless for the same reason.
 //
-// Counting sort over kBuckets weight buckets (integer/byte work, HBM/L2-bound) in two
+// Counting sort over kBuckets weight buckets (integer/byte work, HBM/L2-bound) in three
 // launches with no global atomics (same-address atomics from every workgroup serialise at L2):
 //   hist    : one workgroup per chunk of consecutive syndromes, four threads per syndrome
 //             (16-byte loads along a quarter of its rows, 8 in flight); the workgroup
 //             histograms the buckets in LDS and stores its counts [chunk][bucket]
-//   scatter : each chunk's workgroup derives its own first position in every bucket from the
-//             whole count matrix (bucket totals scanned heaviest-first, plus the counts of the
-//             chunks before it) and places its syndromes (LDS atomics), perm[pos] = b.
-//             (A separate one-workgroup offsets launch was measured at 10.6 us of a 27.7 us
-//             P7 order pass, profiles/r01/session7/rocprof_p7_kernel_stats_s7a.csv.)
+//   offsets : one workgroup per bucket scans its column of the count matrix over the chunks
+//             (each chunk's exclusive prefix, in place) and stores the bucket total;
+//   scatter : each chunk's workgroup scans the 256 totals heaviest-first, adds its own
+//             prefixes, and places its syndromes (LDS atomics), perm[pos] = b.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -113,57 +112,50 @@ __global__ __launch_bounds__(kHistThreads) void schedule_hist_kernel(const uint8
     if (t < kBuckets) counts[(long long)blockIdx.x * kBuckets + t] = h[t];
 }
 
-// Scatter with the offsets computed in place: workgroup c needs, for every bucket k, the
-// total of every heavier bucket (all chunks) plus bucket k's count in chunks before c.  Its
-// kScatSplit threads per bucket each sum a contiguous quarter of the count matrix's rows
-// (coalesced 1 KiB rows, kOffBatch loads in flight), the quarters meet in LDS, and one
-// 256-wide scan turns the totals into bucket starts.  Every workgroup re-reads the whole
-// [chunks][256] matrix (256 KiB at 256 chunks, from L2), which costs less than a separate
-// single-workgroup offsets launch and its gap.  Then its syndromes are placed with LDS atomics.
+// Bucket offsets: workgroup k scans column k of the [chunks][256] count matrix (one thread per
+// chunk, LDS scan), writes each chunk's exclusive prefix in place and the bucket total.  About
+// 2 KiB of the matrix per workgroup; the previous design, every scatter workgroup re-reading
+// the whole matrix, moved 1 GiB through L2 at 2^20 syndromes (1024 chunks): 75 us.
+constexpr int kScanThreads = 1024;  // = kMaxChunks
+__global__ __launch_bounds__(kScanThreads) void schedule_offsets_kernel(int nch, uint32_t* __restrict__ counts,
+                                                                        uint32_t* __restrict__ totals)
+{
+    __shared__ uint32_t v[kScanThreads];
+    const int k = blockIdx.x, c = threadIdx.x;
+    const uint32_t x = c < nch ? counts[(long long)c * kBuckets + k] : 0u;
+    v[c] = x;
+    __syncthreads();
+    for (int o = 1; o < kScanThreads; o <<= 1) {  // inclusive scan over chunks
+        const uint32_t add = c >= o ? v[c - o] : 0u;
+        __syncthreads();
+        v[c] += add;
+        __syncthreads();
+    }
+    if (c < nch) counts[(long long)c * kBuckets + k] = v[c] - x;  // exclusive: syndromes of bucket k in chunks < c
+    if (c == kScanThreads - 1) totals[k] = v[c];
+}
+
+// Scatter: workgroup c scans the 256 bucket totals heaviest-first (its bucket starts), adds its
+// own chunk prefixes, and places its syndromes (LDS atomics), perm[pos] = b.
 constexpr int kScatThreads = 1024;
-constexpr int kScatSplit = kScatThreads / kBuckets;
-constexpr int kOffBatch = 32;
 __global__ __launch_bounds__(kScatThreads) void schedule_scatter_kernel(const uint8_t* __restrict__ key, long long B,
-                                                                      int chunk, int nch,
-                                                                      const uint32_t* __restrict__ counts,
+                                                                      int chunk, const uint32_t* __restrict__ prefix,
+                                                                      const uint32_t* __restrict__ totals,
                                                                       int32_t* __restrict__ perm)
 {
-    __shared__ uint32_t before[kScatSplit][kBuckets];
-    __shared__ uint32_t total[kScatSplit][kBuckets];
+    __shared__ uint32_t start[kBuckets];
     __shared__ uint32_t cur[kBuckets];
     const int t = threadIdx.x;
-    const int k = t % kBuckets, q = t / kBuckets;
     const int c = blockIdx.x;
-    const int c0 = nch * q / kScatSplit, c1 = nch * (q + 1) / kScatSplit;
-    uint32_t pre = 0, all = 0;
-    for (int cb = c0; cb < c1; cb += kOffBatch) {
-        uint32_t v[kOffBatch];
-#pragma unroll
-        for (int j = 0; j < kOffBatch; ++j) v[j] = cb + j < c1 ? counts[(long long)(cb + j) * kBuckets + k] : 0u;
-#pragma unroll
-        for (int j = 0; j < kOffBatch; ++j) {
-            all += v[j];
-            pre += cb + j < c ? v[j] : 0u;
-        }
-    }
-    before[q][k] = pre;
-    total[q][k] = all;
-    __syncthreads();
-    if (q == 0) {
-        uint32_t tot = 0, pb = 0;
-#pragma unroll
-        for (int j = 0; j < kScatSplit; ++j) { tot += total[j][k]; pb += before[j][k]; }
-        total[0][k] = tot;
-        before[0][k] = pb;
-    }
+    if (t < kBuckets) start[t] = totals[t];
     __syncthreads();
     for (int o = 1; o < kBuckets; o <<= 1) {  // inclusive scan of the bucket totals, heaviest first
-        const uint32_t add = (q == 0 && k >= o) ? total[0][k - o] : 0u;
+        const uint32_t add = (t < kBuckets && t >= o) ? start[t - o] : 0u;
         __syncthreads();
-        if (q == 0) total[0][k] += add;
+        if (t < kBuckets) start[t] += add;
         __syncthreads();
     }
-    if (q == 0) cur[k] = (k ? total[0][k - 1] : 0u) + before[0][k];
+    if (t < kBuckets) cur[t] = (t ? start[t - 1] : 0u) + prefix[(long long)c * kBuckets + t];
     __syncthreads();
     const long long r0 = (long long)c * chunk;
     const long long r1 = r0 + chunk < B ? r0 + chunk : B;
@@ -183,12 +175,12 @@ static int chunk_of(long long B, int min_chunk, int* nchunks)
 // B <= kMaxChunks * kMaxChunk syndromes per ordered launch (4 M)
 long long schedule_max_batch() { return (long long)kMaxChunks * kMaxChunk; }
 
-// workspace layout: perm [B] i32, counts [chunks][256] u32, key [B] u8
+// workspace layout: perm [B] i32, counts [chunks][256] u32, totals [256] u32, key [B] u8
 static size_t perm_bytes(long long B) { return ((size_t)B * sizeof(int32_t) + 255) & ~(size_t)255; }
 
 size_t schedule_workspace_bytes(long long B, int, int)
 {
-    return perm_bytes(B) + (size_t)kMaxChunks * kBuckets * 4 + B + 64;
+    return perm_bytes(B) + (size_t)kMaxChunks * kBuckets * 4 + kBuckets * 4 + B + 64;
 }
 
 // Fills the workspace (schedule_workspace_bytes bytes) and returns in *perm_out the
@@ -204,7 +196,8 @@ int launch_schedule(const uint8_t* sX, const uint8_t* sZ, long long B, int mX, i
     uint8_t* p = static_cast<uint8_t*>(ws);
     int32_t* perm = reinterpret_cast<int32_t*>(p);
     uint32_t* counts = reinterpret_cast<uint32_t*>(p + perm_bytes(B));
-    uint8_t* key = reinterpret_cast<uint8_t*>(counts + (size_t)kMaxChunks * kBuckets);
+    uint32_t* totals = counts + (size_t)kMaxChunks * kBuckets;
+    uint8_t* key = reinterpret_cast<uint8_t*>(totals + kBuckets);
     *perm_out = perm;
     if (shortrows)
         hipLaunchKernelGGL(schedule_hist_kernel<1>, dim3(nch), dim3(kHistThreads), 0, st, sX, sZ, B, mX, mZ, chunk, key,
@@ -212,7 +205,8 @@ int launch_schedule(const uint8_t* sX, const uint8_t* sZ, long long B, int mX, i
     else
         hipLaunchKernelGGL(schedule_hist_kernel<kHistSplitLong>, dim3(nch), dim3(kHistThreads), 0, st, sX, sZ, B, mX, mZ,
                            chunk, key, counts, zero_merge);
-    hipLaunchKernelGGL(schedule_scatter_kernel, dim3(nch), dim3(kScatThreads), 0, st, key, B, chunk, nch, counts,
+    hipLaunchKernelGGL(schedule_offsets_kernel, dim3(kBuckets), dim3(kScanThreads), 0, st, nch, counts, totals);
+    hipLaunchKernelGGL(schedule_scatter_kernel, dim3(nch), dim3(kScatThreads), 0, st, key, B, chunk, counts, totals,
                        perm);
     const hipError_t err = hipGetLastError();
     if (err != hipSuccess) return fail(QEC_ERR_HIP, std::string("schedule launch: ") + hipGetErrorString(err));

@@ -17,8 +17,10 @@ def main():
         meta = s[s.index(".amdhsa_kernel " + name):]
         vg = re.search(r"\.amdhsa_next_free_vgpr (\d+)", meta).group(1)
         n = len(re.findall(r"^\s+[vsdgb][a-z_0-9]+ ", body, re.M))
-        print("%-90s instrs %6d vgpr %4s bperm %4d scratch %d" % (
-            name[:90], n, vg, body.count("ds_bpermute"), body.count("scratch_")))
+        short = re.sub(r"GeneratedShifts<.*", "", name)
+        print("%-60s %-8s instrs %6d vgpr %4s bperm %4d scratch %d" % (
+            name[:60], "split" if name.endswith("Lb1EEEvNS_6BpArgsE") else "", n, vg, body.count("ds_bpermute"),
+            body.count("scratch_")))
 
 
 if __name__ == "__main__":

@@ -159,7 +159,8 @@ int qec_decoder_device(const qec_decoder* dec);         /* HIP device ordinal (o
  *     first, so the rare syndromes that run every iteration in full arithmetic start early
  *     instead of extending the launch (schedule.hip).  Outputs are written at each syndrome's
  *     own index and are bit-identical either way.  0 = batch order, 1 = sorted when
- *     4096 <= B <= 2^22, 2 = sorted when B <= 2^22.  The workspace (5 B per syndrome + 1 MiB) is allocated
+ *     4096 <= B <= 2^22 (codes with one syndrome per wave, P > 32: 4096 <= B <= 2^19, above which
+ *     the pass costs more than it saves), 2 = sorted when B <= 2^22.  The workspace (5 B per syndrome + 1 MiB) is allocated
  *     by qec_decoder_create for max_batch and grown on demand by larger calls.
  *   QEC_OPT_SECTOR_SPLIT (default 1): the X and Z sectors of a syndrome are decoded by two
  *     waves instead of one after the other (halves the longest wave).  The launch then zeroes
@@ -236,9 +237,11 @@ typedef struct {
 } qec_mc_result;
 
 /* i.i.d. depolarising errors for samples [start, start+B) of stream `seed` (device buffers
- * x, z: B x n).  Philox4x32-10 with counter (sample lo, sample hi, qubit, 0x51EC0DE5) and key
- * (seed lo, seed hi): the qubit is hit if word0 < floor(p 2^32); its type is (word1 * 3) >> 32
- * (0 = X, 1 = Y, 2 = Z; Y sets both bits).  Any shard of the index space can be drawn alone. */
+ * x, z: B x n).  Philox4x32-10, one call per four qubits: qubits 4g..4g+3 of sample b use counter
+ * (b lo, b hi, g, 0x51EC0DE5) and key (seed lo, seed hi), output word j for qubit 4g + j.  The
+ * qubit is hit if w < thr = floor(p 2^32) (saturated); its type is floor(w mul / 2^64) with
+ * mul = min(floor(3 2^64 / thr), 2^64 - 1): 0 = X, 1 = Y, 2 = Z (each 1/3 to within 1/thr; Y sets
+ * both bits).  Any shard of the index space can be drawn alone. */
 int qec_sample_depolarizing_dev(qec_decoder* dec, uint64_t seed, uint64_t start, size_t B, float p, uint8_t* x,
                                 uint8_t* z, void* stream);
 /* Fused front end: the depolarising errors of qec_sample_depolarizing_dev (same stream, same

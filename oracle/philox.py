@@ -3,9 +3,10 @@
 Philox4x32-10 (Salmon, Moraes, Dror, Shaw, "Parallel random numbers: as easy as
 1, 2, 3", SC'11; the Random123 reference algorithm), pinned by Random123's
 published known-answer vectors (tests/test_philox.py), and the depolarising
-sampler built on it exactly as qec_ldpc_amd/csrc/montecarlo.hip defines it:
-qubit v of sample b uses counter (b_lo, b_hi, v, 0x51EC0DE5) and key
-(seed_lo, seed_hi); hit if word0 < floor(p 2^32) (saturated), type = (word1*3)>>32.
+sampler built on it exactly as qec_ldpc_amd/csrc/montecarlo.hip defines it
+(depolarizing4): qubits 4g..4g+3 of sample b use counter (b_lo, b_hi, g, 0x51EC0DE5)
+and key (seed_lo, seed_hi), word j for qubit 4g + j; hit if w < thr = floor(p 2^32)
+(saturated); type = floor(w mul / 2^64), mul = min(floor(3 2^64 / thr), 2^64 - 1).
 """
 import numpy as np
 
@@ -38,18 +39,30 @@ def threshold(p):
     return int(p * 4294967296.0)
 
 
+def multiplier(thr):
+    """mul = min(floor(3 2^64 / thr), 2^64 - 1) (0 for thr = 0)."""
+    if thr == 0:
+        return 0
+    return min((3 << 64) // thr, (1 << 64) - 1)
+
+
 def depolarizing(seed, start, count, n, p):
     """(x, z) uint8 [count, n] for samples [start, start+count) of stream `seed`."""
+    ng = (n + 3) // 4
     b = np.arange(start, start + count, dtype=np.uint64)[:, None]
-    v = np.arange(n, dtype=np.uint64)[None, :]
-    shape = (count, n)
+    g = np.arange(ng, dtype=np.uint64)[None, :]
+    shape = (count, ng)
     c0 = np.broadcast_to(b & MASK, shape)
     c1 = np.broadcast_to(b >> np.uint64(32), shape)
-    c2 = np.broadcast_to(v, shape)
+    c2 = np.broadcast_to(g, shape)
     c3 = np.full(shape, SALT, dtype=np.uint64)
-    w0, w1, _, _ = philox4x32_10(c0, c1, c2, c3, seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF)
-    hit = w0.astype(np.uint64) < np.uint64(threshold(p)) if threshold(p) < (1 << 32) else np.ones(shape, bool)
-    typ = ((w1.astype(np.uint64) * np.uint64(3)) >> np.uint64(32)).astype(np.uint8)
+    words = philox4x32_10(c0, c1, c2, c3, seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF)
+    w = np.stack(words, axis=2).reshape(count, 4 * ng)[:, :n].astype(np.uint64)  # word j -> qubit 4g + j
+    thr = threshold(p)
+    mul = multiplier(thr)
+    hit = w < np.uint64(thr) if thr < (1 << 32) else np.ones(w.shape, bool)
+    hi = w * np.uint64(mul >> 32) + ((w * np.uint64(mul & 0xFFFFFFFF)) >> np.uint64(32))
+    typ = (hi >> np.uint64(32)).astype(np.uint8)
     x = (hit & (typ != 2)).astype(np.uint8)
     z = (hit & (typ != 0)).astype(np.uint8)
     return x, z

@@ -429,9 +429,14 @@ int qec_decoder_get_option(const qec_decoder* d, int option, int* value)
 
 namespace {
 
-// QEC_OPT_SCHEDULE = 1 orders batches from this size on (below it the two extra launches
-// cost more than the tail they remove)
+// QEC_OPT_SCHEDULE = 1 orders batches from this size on (below it the extra launches cost more
+// than the tail they remove) and, with one syndrome per wave (P > 32), up to kScheduleMaxSingle:
+// there the order pass reads every syndrome once more (P61: 177 us per 2^20) while the tail it
+// removes stays about one long sector (~0.1 ms); P61 at 2^20: 118.7 M/s unordered vs 116.9 M/s,
+// at 131 072: 101 M/s vs 113 M/s (profiles/r02/ab_schedule.txt).  Several syndromes per wave (P7)
+// always gain: similar syndromes then share waves (1.56 G/s vs 0.88 G/s at 2^20).
 constexpr long long kScheduleMinBatch = 4096;
+constexpr long long kScheduleMaxSingle = 1LL << 19;
 
 // One decode launch of a single-device handle on device buffers.  Outputs: byte form (eX, eZ,
 // flags) or, with rec non-null, the packed decision records.
@@ -460,7 +465,9 @@ int dispatch_decode(qec_decoder* d, const uint8_t* sX, const uint8_t* sZ, long l
     if (split && (rc = ws_reserve(d->merge, (size_t)B, st, "decode"))) return rc;
     const int32_t* perm = nullptr;
     bool zeroed = false;
-    if (B > 1 && B <= schedule_max_batch() && (d->schedule == 2 || (d->schedule == 1 && B >= kScheduleMinBatch))) {
+    const bool single = 2 * c.P > 64;  // one syndrome per wave
+    const bool auto_on = B >= kScheduleMinBatch && (!single || B <= kScheduleMaxSingle);
+    if (B > 1 && B <= schedule_max_batch() && (d->schedule == 2 || (d->schedule == 1 && auto_on))) {
         if ((rc = ws_reserve(d->sched, schedule_workspace_bytes(B, c.mX, c.mZ), st, "decode: dispatch order")))
             return rc;
         int32_t* pm = nullptr;

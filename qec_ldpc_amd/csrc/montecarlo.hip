@@ -14,6 +14,7 @@
 // These are integer/byte kernels: HBM/L2-bound, not worth MFMA.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 
 #include "qec_device.h"
@@ -42,23 +43,69 @@ __host__ __device__ inline U4 philox4x32_10(U4 c, uint32_t k0, uint32_t k1)
 
 constexpr uint32_t kPhiloxSalt = 0x51EC0DE5u;
 
-// Qubit v of sample b: counter (b_lo, b_hi, v, salt), key (seed_lo, seed_hi).
-// word x: hit if x < thr (thr = floor(p 2^32), saturated); word y: type = (y * 3) >> 32,
-// 0 = X, 1 = Y, 2 = Z.  Restated in numpy by qec_ldpc_amd/synthetic.py.
-__global__ void sample_depolarizing_kernel(uint64_t seed, uint64_t start, long long B, int n, uint64_t thr,
-                                           uint8_t* __restrict__ x, uint8_t* __restrict__ z)
+// Depolarising sampler.  Qubits 4g .. 4g+3 of sample b share one Philox call: counter
+// (b_lo, b_hi, g, salt), key (seed_lo, seed_hi), output words w0..w3, word j for qubit 4g + j.
+// The qubit is hit iff w < thr = floor(p 2^32) (saturated at 2^32).  Given a hit, w is uniform on
+// [0, thr), and its type is t = floor(w mul / 2^64) with mul = min(floor(3 2^64 / thr), 2^64 - 1),
+// i.e. floor(3 w / thr) up to the rounding of mul: 0 = X, 1 = Y, 2 = Z, each with probability
+// 1/3 to within 1/thr (Y sets both bits).  Four qubits per call: the front end's cost is the
+// Philox rounds.  Restated in numpy by oracle/philox.py.
+struct Depol {
+    uint64_t seed, thr, mul;
+};
+
+__host__ inline Depol make_depol(uint64_t seed, float p)
 {
+    const double pd = p;
+    Depol d{seed, pd <= 0.0 ? 0ull : pd >= 1.0 ? (1ull << 32) : (uint64_t)(pd * 4294967296.0), 0};
+    if (d.thr >= 3) {
+        const unsigned __int128 m = ((unsigned __int128)3 << 64) / d.thr;
+        d.mul = m > ~0ull ? ~0ull : (uint64_t)m;
+    } else if (d.thr > 0) {
+        d.mul = ~0ull;
+    }
+    return d;
+}
+
+// x4 / z4: the four qubits' bits as bytes (byte j = qubit 4g + j)
+__device__ __forceinline__ void depolarizing4(const Depol& d, uint64_t sb, uint32_t g, uint32_t& x4, uint32_t& z4)
+{
+    const U4 o = philox4x32_10(U4{(uint32_t)sb, (uint32_t)(sb >> 32), g, kPhiloxSalt}, (uint32_t)d.seed,
+                               (uint32_t)(d.seed >> 32));
+    const uint32_t w[4] = {o.x, o.y, o.z, o.w};
+    x4 = 0;
+    z4 = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        if ((uint64_t)w[j] < d.thr) {
+            // floor(w mul / 2^64) = floor((w mul_hi + floor(w mul_lo / 2^32)) / 2^32), no overflow
+            const uint64_t hi = (uint64_t)w[j] * (d.mul >> 32) + (((uint64_t)w[j] * (uint32_t)d.mul) >> 32);
+            const uint32_t t = (uint32_t)(hi >> 32);
+            x4 |= (uint32_t)(t != 2) << (8 * j);
+            z4 |= (uint32_t)(t != 0) << (8 * j);
+        }
+    }
+}
+
+// byte form (qec_sample_depolarizing_dev): one thread per four qubits of a sample
+__global__ void sample_depolarizing_kernel(Depol d, uint64_t start, long long B, int n, uint8_t* __restrict__ x,
+                                           uint8_t* __restrict__ z)
+{
+    const int ng = (n + 3) / 4;
     const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= B * n) return;
-    const long long b = t / n;
-    const int v = (int)(t - b * n);
-    const uint64_t sb = start + (uint64_t)b;
-    const U4 o = philox4x32_10(U4{(uint32_t)sb, (uint32_t)(sb >> 32), (uint32_t)v, kPhiloxSalt}, (uint32_t)seed,
-                               (uint32_t)(seed >> 32));
-    const bool hit = (uint64_t)o.x < thr;
-    const uint32_t type = (uint32_t)(((uint64_t)o.y * 3u) >> 32);
-    x[t] = (uint8_t)(hit && type != 2);
-    z[t] = (uint8_t)(hit && type != 0);
+    if (t >= B * ng) return;
+    const long long b = t / ng;
+    const int g = (int)(t - b * ng);
+    uint32_t x4, z4;
+    depolarizing4(d, start + (uint64_t)b, (uint32_t)g, x4, z4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int v = 4 * g + j;
+        if (v < n) {
+            x[b * n + v] = (uint8_t)((x4 >> (8 * j)) & 1u);
+            z[b * n + v] = (uint8_t)((z4 >> (8 * j)) & 1u);
+        }
+    }
 }
 
 // counters, in qec_mc_counters order
@@ -167,7 +214,8 @@ constexpr int kMcWaves = 4;
 
 struct McArgs {
     // sources
-    uint64_t seed, start, thr;                 // PHILOX
+    Depol depol;                               // PHILOX
+    uint64_t start;
     const int32_t* idx;                        // DRAWS: [B][W] qubit indices
     const uint8_t* type;                       //        [B][W] 0 = X, 1 = Y, 2 = Z
     int W;
@@ -179,76 +227,114 @@ struct McArgs {
     uint8_t* errp;                             // [B][2 nb] (nullable)
     const int32_t* chkVar;                     // non-QC codes: [(mX + mZ) L] variables per check
     long long B;
-    int n, nb, L, P, mX, mZ;
+    int n, nb, L, P, J, K, mX, mZ;
+    int S;                                     // samples per wave
+    uint32_t magicW, magicG, magicN, magicM, magicP, magicB;  // ceil(2^32 / d) for the item counts
     int EX[128], EZ[128];
 };
 
+// (i, k) = (t / d, t mod d) for the small work-item counts below: magic = ceil(2^32 / d) is exact
+// for t d < 2^32 (t < 2^16 and d < 2^16 here)
+__device__ __forceinline__ int qdiv(int t, uint32_t magic) { return (int)__umulhi((uint32_t)t, magic); }
+
+// A wave handles S = max(1, floor(64 / P)) samples (P61: 1, P7: 9), so short codes keep the lanes
+// busy; each phase spreads its (sample, item) pairs over the lanes.
 template <int SRC>
 __global__ __launch_bounds__(64 * kMcWaves) void mc_errors_syndrome_kernel(const McArgs a)
 {
     extern __shared__ __attribute__((aligned(8))) uint8_t mc_smem[];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const long long b = (long long)blockIdx.x * kMcWaves + wv;
-    if (b >= a.B) return;  // wave-local from here on: no workgroup barrier
+    const int S = a.S;
+    const long long b0 = ((long long)blockIdx.x * kMcWaves + wv) * S;
+    if (b0 >= a.B) return;  // wave-local from here on: no workgroup barrier
+    const int ns = (int)(a.B - b0 < S ? a.B - b0 : S);  // samples of this wave
     const int n = a.n, npad = 8 * a.nb;
-    uint8_t* __restrict__ ex = mc_smem + (size_t)wv * 2 * npad;
-    uint8_t* __restrict__ ez = ex + npad;
+    uint8_t* __restrict__ stage = mc_smem + (size_t)wv * S * 2 * npad;  // sample s: x at 2 s npad, z after
     if constexpr (SRC == MC_SRC_DRAWS) {
-        for (int v = lane; v < npad; v += 64) { ex[v] = 0; ez[v] = 0; }
+        const int nw = npad / 4;  // zero both rows, a word at a time
+        for (int t = lane; t < ns * 2 * nw; t += 64) reinterpret_cast<uint32_t*>(stage)[t] = 0u;
         wave_sync();
-        for (int w = lane; w < a.W; w += 64) {
+        for (int t = lane; t < ns * a.W; t += 64) {
+            const int sI = qdiv(t, a.magicW), w = t - sI * a.W;
+            const long long b = b0 + sI;
             const int v = a.idx[b * a.W + w];
-            const int t = a.type[b * a.W + w];
-            if (t == 0 || t == 1) ex[v] = 1;  // several draws may hit one qubit: they all store 1
-            if (t == 2 || t == 1) ez[v] = 1;
+            const int ty = a.type[b * a.W + w];
+            uint8_t* ex = stage + (size_t)sI * 2 * npad;
+            if (ty == 0 || ty == 1) ex[v] = 1;  // several draws may hit one qubit: they all store 1
+            if (ty == 2 || ty == 1) ex[npad + v] = 1;
         }
-    } else {
-        for (int v = lane; v < npad; v += 64) {
-            uint8_t xv = 0, zv = 0;
-            if (v < n) {
-                if constexpr (SRC == MC_SRC_PHILOX) {
-                    const uint64_t sb = a.start + (uint64_t)b;
-                    const U4 o = philox4x32_10(U4{(uint32_t)sb, (uint32_t)(sb >> 32), (uint32_t)v, kPhiloxSalt},
-                                               (uint32_t)a.seed, (uint32_t)(a.seed >> 32));
-                    const bool hit = (uint64_t)o.x < a.thr;
-                    const uint32_t type = (uint32_t)(((uint64_t)o.y * 3u) >> 32);
-                    xv = (uint8_t)(hit && type != 2);
-                    zv = (uint8_t)(hit && type != 0);
-                } else {
-                    xv = a.x[b * n + v] & 1u;
-                    zv = a.z[b * n + v] & 1u;
+    } else if constexpr (SRC == MC_SRC_PHILOX) {
+        // four qubits per lane and Philox call, one 32-bit LDS word per row (npad is a multiple of
+        // 8, so the padding words are written too, zero past n)
+        const int ng = npad / 4;
+        for (int t = lane; t < ns * ng; t += 64) {
+            const int sI = qdiv(t, a.magicG), g = t - sI * ng;
+            uint32_t x4 = 0, z4 = 0;
+            if (4 * g < n) {
+                depolarizing4(a.depol, a.start + (uint64_t)(b0 + sI), (uint32_t)g, x4, z4);
+                if (4 * g + 4 > n) {
+                    const uint32_t keep = 0xFFFFFFFFu >> (8 * (4 * g + 4 - n));
+                    x4 &= keep;
+                    z4 &= keep;
                 }
             }
-            ex[v] = xv;
-            ez[v] = zv;
+            uint32_t* row = reinterpret_cast<uint32_t*>(stage + (size_t)sI * 2 * npad);
+            row[g] = x4;
+            row[ng + g] = z4;
+        }
+    } else {
+        for (int t = lane; t < ns * npad; t += 64) {
+            const int sI = qdiv(t, a.magicN), v = t - sI * npad;
+            uint8_t xv = 0, zv = 0;
+            if (v < n) {
+                const long long b = b0 + sI;
+                xv = a.x[b * n + v] & 1u;
+                zv = a.z[b * n + v] & 1u;
+            }
+            stage[(size_t)sI * 2 * npad + v] = xv;
+            stage[(size_t)sI * 2 * npad + npad + v] = zv;
         }
     }
     wave_sync();
-    const int m = a.mX + a.mZ;
-    for (int c = lane; c < m; c += 64) {
-        const bool zs = c >= a.mX;
-        const int cc = zs ? c - a.mX : c;
-        const uint8_t* e = zs ? ez : ex;
-        uint32_t s = 0;
-        if (a.chkVar != nullptr) {
+    if (a.chkVar != nullptr) {  // any regular code: the check's variables from the sparse engine's table
+        const int m = a.mX + a.mZ;
+        for (int t = lane; t < ns * m; t += 64) {
+            const int sI = qdiv(t, a.magicM), c = t - sI * m;
+            const bool zs = c >= a.mX;
+            const uint8_t* e = stage + (size_t)sI * 2 * npad + (zs ? npad : 0);
             const int32_t* vars = a.chkVar + (size_t)c * a.L;
-            for (int k = 0; k < a.L; ++k) s ^= e[vars[k]];
-        } else {
-            const int r = cc / a.P, i = cc - r * a.P;
-            const int* E = zs ? a.EZ : a.EX;
-            for (int l = 0; l < a.L; ++l) {
-                int j = E[r * a.L + l] + i;
-                j -= (j >= a.P) ? a.P : 0;
-                s ^= e[l * a.P + j];
+            uint32_t x = 0;
+            for (int k = 0; k < a.L; ++k) x ^= e[vars[k]];
+            const long long b = b0 + sI;
+            if (zs) a.sZ[b * a.mZ + (c - a.mX)] = (uint8_t)(x & 1u); else a.sX[b * a.mX + c] = (uint8_t)(x & 1u);
+        }
+    } else {  // QC: lane (sample, i) computes checks (r, i) of every block row; E[r][l] is uniform
+        const int P = a.P, L = a.L;
+        for (int t = lane; t < ns * P; t += 64) {
+            const int sI = qdiv(t, a.magicP), i = t - sI * P;
+            const long long b = b0 + sI;
+            const uint8_t* ex = stage + (size_t)sI * 2 * npad;
+            for (int r = 0; r < a.J + a.K; ++r) {
+                const bool zs = r >= a.J;
+                const uint8_t* e = zs ? ex + npad : ex;
+                const int* E = zs ? a.EZ + (r - a.J) * L : a.EX + r * L;
+                uint32_t x = 0;
+                for (int l = 0; l < L; ++l) {
+                    int j = E[l] + i;
+                    j -= (j >= P) ? P : 0;
+                    x ^= e[l * P + j];
+                }
+                if (zs) a.sZ[b * a.mZ + (r - a.J) * P + i] = (uint8_t)(x & 1u);
+                else a.sX[b * a.mX + r * P + i] = (uint8_t)(x & 1u);
             }
         }
-        (zs ? a.sZ + b * a.mZ : a.sX + b * a.mX)[cc] = (uint8_t)(s & 1u);
     }
     if (a.errp != nullptr) {
-        for (int t = lane; t < 2 * a.nb; t += 64) {
-            const int k = t < a.nb ? t : t - a.nb;
-            const uint8_t* e = t < a.nb ? ex : ez;
-            a.errp[b * 2 * a.nb + t] = (uint8_t)pack8(*reinterpret_cast<const uint64_t*>(e + 8 * k));
+        const int nb2 = 2 * a.nb;
+        for (int t = lane; t < ns * nb2; t += 64) {
+            const int sI = qdiv(t, a.magicB), k = t - sI * nb2;  // byte k of [x bits | z bits]
+            const uint8_t* e = stage + (size_t)sI * 2 * npad + (k < a.nb ? 8 * k : npad + 8 * (k - a.nb));
+            a.errp[(b0 + sI) * nb2 + k] = (uint8_t)pack8(*reinterpret_cast<const uint64_t*>(e));
         }
     }
 }
@@ -331,11 +417,9 @@ int launch_sample_depolarizing(uint64_t seed, uint64_t start, long long B, int n
                                hipStream_t st)
 {
     if (B <= 0) return QEC_OK;
-    const double pd = p;
-    const uint64_t thr = pd <= 0.0 ? 0ull : pd >= 1.0 ? (1ull << 32) : (uint64_t)(pd * 4294967296.0);
-    const long long tot = B * n;
-    hipLaunchKernelGGL(sample_depolarizing_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, seed, start, B,
-                       n, thr, x, z);
+    const long long tot = B * ((n + 3) / 4);
+    hipLaunchKernelGGL(sample_depolarizing_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st,
+                       make_depol(seed, p), start, B, n, x, z);
     return launch_check("sample_depolarizing");
 }
 
@@ -344,23 +428,31 @@ int launch_mc_errors_syndrome(int src, const McArgsHost& h, hipStream_t st)
     if (h.B <= 0) return QEC_OK;
     const Code& c = *h.code;
     McArgs a{};
-    a.seed = h.seed; a.start = h.start;
-    const double pd = h.p;
-    a.thr = pd <= 0.0 ? 0ull : pd >= 1.0 ? (1ull << 32) : (uint64_t)(pd * 4294967296.0);
+    a.depol = make_depol(h.seed, h.p);
+    a.start = h.start;
     a.idx = h.idx; a.type = h.type; a.W = h.W;
     a.x = h.x; a.z = h.z;
     a.sX = h.sX; a.sZ = h.sZ; a.errp = h.errp;
     a.chkVar = h.chkVar;
     a.B = h.B;
-    a.n = c.n; a.nb = (c.n + 7) / 8; a.L = c.L; a.P = c.P; a.mX = c.mX; a.mZ = c.mZ;
+    a.n = c.n; a.nb = (c.n + 7) / 8; a.L = c.L; a.P = c.P; a.J = c.J; a.K = c.K; a.mX = c.mX; a.mZ = c.mZ;
     if (a.chkVar == nullptr) {
         if (!c.is_qc || c.J * c.L > 128 || c.K * c.L > 128) return fail(QEC_ERR_UNSUPPORTED, "mc front end: needs a QC code or a check table");
         for (size_t k = 0; k < c.EX.size(); ++k) a.EX[k] = c.EX[k];
         for (size_t k = 0; k < c.EZ.size(); ++k) a.EZ[k] = c.EZ[k];
     }
-    const size_t smem = (size_t)kMcWaves * 2 * 8 * a.nb;
+    const int npad = 8 * a.nb;
+    a.S = (a.chkVar == nullptr && c.P > 0 && c.P < 64) ? 64 / c.P : 1;
+    if ((size_t)a.S * 2 * npad > 4096) a.S = 1;
+    auto magic = [](long long d) { return d > 0 ? (uint32_t)(((1ull << 32) + (uint64_t)d - 1) / (uint64_t)d) : 0u; };
+    a.magicW = magic(h.W); a.magicG = magic(npad / 4); a.magicN = magic(npad); a.magicM = magic(c.mX + c.mZ);
+    a.magicP = magic(c.P); a.magicB = magic(2 * a.nb);
+    if ((long long)a.S * std::max<long long>({(long long)h.W, npad, (long long)c.mX + c.mZ}) >= 65536)
+        return fail(QEC_ERR_UNSUPPORTED, "mc front end: code too long");
+    const size_t smem = (size_t)kMcWaves * a.S * 2 * npad;
     if (smem > 64 * 1024) return fail(QEC_ERR_UNSUPPORTED, "mc front end: code too long for the LDS stage");
-    const dim3 grid((unsigned)((h.B + kMcWaves - 1) / kMcWaves)), block(64 * kMcWaves);
+    const long long per_block = (long long)kMcWaves * a.S;
+    const dim3 grid((unsigned)((h.B + per_block - 1) / per_block)), block(64 * kMcWaves);
     if (src == MC_SRC_PHILOX)
         hipLaunchKernelGGL(mc_errors_syndrome_kernel<MC_SRC_PHILOX>, grid, block, smem, st, a);
     else if (src == MC_SRC_DRAWS)

@@ -77,12 +77,13 @@ def main():
         r = dec.monte_carlo(args.seed, lo, hi - lo, p, args.iters, args.stop, args.batch)
         dt = time.perf_counter() - t0
         vec = torch.tensor([r[k] for k in FIELDS], dtype=torch.int64, device=dev)
-        tm = torch.tensor([dt], dtype=torch.float64, device=dev)
+        tm = torch.tensor([dt, r["decodeSeconds"]], dtype=torch.float64, device=dev)
         if world > 1:
             dist.all_reduce(vec)
             dist.all_reduce(tm, op=dist.ReduceOp.MAX)
         c = dict(zip(FIELDS, vec.cpu().tolist()))
-        line = summarize(p, c, float(tm.item()), world)
+        line = summarize(p, c, float(tm[0].item()), world)
+        line["decode_seconds"] = round(float(tm[1].item()), 4)  # decode kernels only (the rest: front end + counts)
         line.update({"code": code.describe(), "stop": args.stop, "max_iters": args.iters, "seed": args.seed})
         lines.append(line)
         if rank == 0:

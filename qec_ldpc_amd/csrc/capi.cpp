@@ -28,7 +28,7 @@ bool decode_has_phase_stats(const void* variant, int stop);
 int launch_sample_depolarizing(uint64_t seed, uint64_t start, long long B, int n, float p, uint8_t* x, uint8_t* z,
                                hipStream_t st);
 int launch_mc_errors_syndrome(int src, const McArgsHost& h, hipStream_t st);
-int launch_statistics_packed(const Code& c, const uint64_t* imp_rec_dev, const uint8_t* errp, const uint8_t* rec,
+int launch_statistics_packed(const Code& c, const uint64_t* imp_cols, const uint8_t* errp, const uint8_t* rec,
                              const int32_t* iters, long long B, unsigned long long* counters, hipStream_t st);
 void* sparse_plan_create(const Code& c, int device);
 void sparse_plan_free(void* plan);
@@ -39,7 +39,7 @@ int launch_decode_sparse(void* plan, const uint8_t* sX, const uint8_t* sZ, long 
                          hipStream_t stream);
 int launch_pack_decisions(const uint8_t* eX, const uint8_t* eZ, const uint8_t* flags, long long B, int n, uint8_t* out,
                           hipStream_t st);
-int launch_statistics(const Code& c, const uint64_t* imp_dev, const uint8_t* x, const uint8_t* z, const uint8_t* eX,
+int launch_statistics(const Code& c, const uint64_t* imp_cols, const uint8_t* x, const uint8_t* z, const uint8_t* eX,
                       const uint8_t* eZ, const uint8_t* flags, long long B, unsigned long long* counters, hipStream_t st);
 }  // namespace qec
 
@@ -78,8 +78,7 @@ struct qec_decoder {
     DeviceArray<int32_t> iters;
     DeviceArray<float> q;
     // Monte-Carlo workspace (qec_monte_carlo / qec_get_statistics)
-    DeviceArray<uint64_t> imp;      // bit-packed non-zero I-P rows, qubit layout (statistics_kernel)
-    DeviceArray<uint64_t> imp_rec;  // the same rows in the decision-record layout (statistics_packed_kernel)
+    DeviceArray<uint64_t> imp_cols;  // I-P by columns over its non-zero rows (Code::imp_cols)
     DeviceArray<uint8_t> msX, msZ, merrp, mrec, mtype;
     DeviceArray<int32_t> mit, midx;
     DeviceArray<unsigned long long> mcount;
@@ -315,13 +314,10 @@ qec_decoder* qec_decoder_create_engine(const qec_code* h, int device, size_t max
             d->eZ.reserve(max_batch * d->code->n);
             d->flags.reserve(max_batch);
         }
-        if (!d->code->imp_rows.empty()) {
-            d->imp.reserve(d->code->imp_rows.size());
-            hip_throw(hipMemcpy(d->imp.data(), d->code->imp_rows.data(), d->code->imp_rows.size() * sizeof(uint64_t),
+        if (!d->code->imp_cols.empty()) {
+            d->imp_cols.reserve(d->code->imp_cols.size());
+            hip_throw(hipMemcpy(d->imp_cols.data(), d->code->imp_cols.data(), d->code->imp_cols.size() * sizeof(uint64_t),
                                 hipMemcpyHostToDevice), "I-P upload");
-            d->imp_rec.reserve(d->code->imp_rows_rec.size());
-            hip_throw(hipMemcpy(d->imp_rec.data(), d->code->imp_rows_rec.data(),
-                                d->code->imp_rows_rec.size() * sizeof(uint64_t), hipMemcpyHostToDevice), "I-P upload");
         }
         d->mcount.reserve(QEC_MC_NCOUNTERS_ALL);
     } catch (const std::exception& ex) {
@@ -670,7 +666,7 @@ int mc_batch(qec_decoder* d, McArgsHost h, int src, float p, int maxIter, int st
                          d->mrec.data(), want_iters ? d->mit.data() : nullptr, nullptr, st);
     if (rc) return rc;
     if (ev1) QEC_HIP_CHECK(hipEventRecord(ev1, st));
-    return launch_statistics_packed(*d->code, d->imp_rec.data(), d->merrp.data(), d->mrec.data(),
+    return launch_statistics_packed(*d->code, d->imp_cols.data(), d->merrp.data(), d->mrec.data(),
                                     want_iters ? d->mit.data() : nullptr, h.B, d->mcount.data(), st);
 }
 
@@ -939,7 +935,7 @@ int qec_statistics_dev(qec_decoder* d, const uint8_t* x, const uint8_t* z, const
     int rc = single_device_only(d, "qec_statistics_dev");
     if (rc) return rc;
     QEC_DEVICE_SCOPE(d->device);
-    return launch_statistics(*d->code, d->imp.data(), x, z, eX, eZ, flags, (long long)B,
+    return launch_statistics(*d->code, d->imp_cols.data(), x, z, eX, eZ, flags, (long long)B,
                              reinterpret_cast<unsigned long long*>(counters), static_cast<hipStream_t>(stream));
 }
 
@@ -951,7 +947,7 @@ int qec_statistics_packed_dev(qec_decoder* d, const uint8_t* errp, const uint8_t
     int rc = single_device_only(d, "qec_statistics_packed_dev");
     if (rc) return rc;
     QEC_DEVICE_SCOPE(d->device);
-    return launch_statistics_packed(*d->code, d->imp_rec.data(), errp, records, iters, (long long)B,
+    return launch_statistics_packed(*d->code, d->imp_cols.data(), errp, records, iters, (long long)B,
                                     reinterpret_cast<unsigned long long*>(counters), static_cast<hipStream_t>(stream));
 }
 

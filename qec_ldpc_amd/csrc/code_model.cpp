@@ -103,22 +103,20 @@ void finalize_code(Code& c)
                 if (c.imp[(size_t)i * N2 + j]) { row[j >> 6] |= 1ull << (j & 63); any = true; }
             if (any) c.imp_rows.insert(c.imp_rows.end(), row.begin(), row.end());
         }
-        // the same rows in the decision-record bit layout (x qubit q at bit q, z qubit t at bit
-        // 8 nb + t, nb = ceil(n / 8)), so a packed residual [x ^ eX | z ^ eZ] is tested as it stands
-        const int nb = (c.n + 7) / 8;
-        c.imp_words_rec = (2 * nb + 7) / 8;
-        c.imp_rows_rec.clear();
-        std::vector<uint64_t> rr(c.imp_words_rec);
+        // the same test column by column: (I-P) r != 0 iff the XOR of the columns of I-P at the set
+        // bits of r, restricted to its non-zero rows, is non-zero.  A decoded residual is almost
+        // always 0 or sparse, so the device kernels touch a few columns instead of every row.
+        const int nrows = c.imp_words ? (int)(c.imp_rows.size() / c.imp_words) : 0;
+        c.imp_col_words = (nrows + 63) / 64;
+        c.imp_cols.assign((size_t)N2 * c.imp_col_words, 0);
+        int k = 0;
         for (int i = 0; i < N2; ++i) {
-            std::fill(rr.begin(), rr.end(), 0);
             bool any = false;
+            for (int j = 0; j < N2 && !any; ++j) any = c.imp[(size_t)i * N2 + j] != 0;
+            if (!any) continue;
             for (int j = 0; j < N2; ++j)
-                if (c.imp[(size_t)i * N2 + j]) {
-                    const int bit = j < c.n ? j : 8 * nb + (j - c.n);
-                    rr[bit >> 6] |= 1ull << (bit & 63);
-                    any = true;
-                }
-            if (any) c.imp_rows_rec.insert(c.imp_rows_rec.end(), rr.begin(), rr.end());
+                if (c.imp[(size_t)i * N2 + j]) c.imp_cols[(size_t)j * c.imp_col_words + (k >> 6)] |= 1ull << (k & 63);
+            ++k;
         }
     }
 }

@@ -111,16 +111,42 @@ __global__ void sample_depolarizing_kernel(Depol d, uint64_t start, long long B,
 // counters, in qec_mc_counters order
 enum { C_WITHX, C_WITHZ, C_SYNX, C_SYNZ, C_LOGICAL, C_CORRECTED, C_CONVX, C_CONVZ, C_N };
 
-// One wave per sample.  Residual words are formed with ballots (lane = qubit within a
-// 64-qubit word) and parked in LDS, so every lane can test its share of the non-zero
-// I-P rows (bit-packed, imp_words u64 per row) for odd parity against them.
+// CheckLogicalError (Quantum_LDPC_Code.h:126-142): (I-P) r != 0 for the residual r, as the XOR
+// of the columns of I-P (restricted to its non-zero rows, cw <= 64 words each; lane k holds word
+// k of the sum) at the set bits of r.  A decoded residual is nearly always 0 or sparse, so this
+// reads a few columns instead of every row (P61: 678 x 20 words per sample).  res[0..nw) is the
+// residual in LDS, the same for every lane; REC: record layout (x bits at [0, 8 nb), z bits at
+// [8 nb, 16 nb)), else qubit layout (bit q = qubit q of [x | z]).
 constexpr int kStatWaves = 4;
 constexpr int kMaxWords = 64;  // 2n <= 4096 qubits
+
+template <bool REC>
+__device__ __forceinline__ bool logical_from_columns(const unsigned long long* res, int nw, int n, int nb,
+                                                     const uint64_t* __restrict__ cols, int cw, int lane)
+{
+    uint64_t acc = 0;
+    for (int w = 0; w < nw; ++w) {
+        const uint64_t v = res[w];
+        uint64_t bits = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32) |
+                        __builtin_amdgcn_readfirstlane((uint32_t)v);  // uniform: scalar loop below
+        while (bits) {
+            const int j = __builtin_ctzll(bits);
+            bits &= bits - 1;
+            int q = 64 * w + j;
+            if (REC) q = q < 8 * nb ? q : n + (q - 8 * nb);
+            if (lane < cw) acc ^= cols[(size_t)q * cw + lane];
+        }
+    }
+    return __any(acc != 0);
+}
+
+// One wave per sample.  Residual words are formed with ballots (lane = qubit within a
+// 64-qubit word) and parked in LDS for the column test above.
 
 __global__ __launch_bounds__(64 * kStatWaves) void statistics_kernel(
     const uint8_t* __restrict__ x, const uint8_t* __restrict__ z, const uint8_t* __restrict__ eX,
     const uint8_t* __restrict__ eZ, const uint8_t* __restrict__ flags, long long B, int n,
-    const uint64_t* __restrict__ imp_rows, int imp_nrows, int imp_words, unsigned long long* __restrict__ counters)
+    const uint64_t* __restrict__ imp_cols, int imp_cw, unsigned long long* __restrict__ counters)
 {
     __shared__ unsigned long long part[C_N];
     __shared__ unsigned long long sres[kStatWaves][kMaxWords];
@@ -153,16 +179,8 @@ __global__ __launch_bounds__(64 * kStatWaves) void statistics_kernel(
         const bool wx = __any(anyX), wz = __any(anyZ);
         const bool dEX = f & QEC_SYNDROME_FAIL_X, dEZ = f & QEC_SYNDROME_FAIL_Z;
         bool logical = false;
-        if (!(dEX || dEZ) && imp_nrows > 0) {  // CheckLogicalError only when no syndrome failure
-            bool odd = false;
-            for (int row = lane; row < imp_nrows; row += 64) {
-                const uint64_t* rp = imp_rows + (size_t)row * imp_words;
-                unsigned long long acc = 0;
-                for (int w = 0; w < imp_words; ++w) acc ^= rp[w] & sres[wv][w];
-                odd |= (__popcll(acc) & 1) != 0;
-            }
-            logical = __any(odd);
-        }
+        if (!(dEX || dEZ) && imp_cw > 0)  // CheckLogicalError only when no syndrome failure
+            logical = logical_from_columns<false>(sres[wv], nw, n, 0, imp_cols, imp_cw, lane);
         if (lane == 0) {
             atomicAdd(&part[C_WITHX], (unsigned long long)wx);
             atomicAdd(&part[C_WITHZ], (unsigned long long)wz);
@@ -234,8 +252,8 @@ struct McArgs {
 };
 
 // (i, k) = (t / d, t mod d) for the small work-item counts below: magic = ceil(2^32 / d) is exact
-// for t d < 2^32 (t < 2^16 and d < 2^16 here)
-__device__ __forceinline__ int qdiv(int t, uint32_t magic) { return (int)__umulhi((uint32_t)t, magic); }
+// for t d < 2^32 (t < 2^16 and d < 2^16 here); d = 1 (magic 2^32 does not fit) is passed as 0
+__device__ __forceinline__ int qdiv(int t, uint32_t magic) { return magic ? (int)__umulhi((uint32_t)t, magic) : t; }
 
 // A wave handles S = max(1, floor(64 / P)) samples (P61: 1, P7: 9), so short codes keep the lanes
 // busy; each phase spreads its (sample, item) pairs over the lanes.
@@ -341,14 +359,14 @@ __global__ __launch_bounds__(64 * kMcWaves) void mc_errors_syndrome_kernel(const
 
 // CodeStatistics counters of a batch from bit-packed errors errp [B][2 nb] and decision records
 // rec [B][2 nb + 1] (qec_decode_batch_packed_dev): the residual [x ^ eX | z ^ eZ] is their XOR
-// over the first 2 nb bytes, tested against the I-P rows packed in the same layout
-// (Code::imp_rows_rec); optional iteration sums (iters [B][2]) into counters[8], counters[9].
+// over the first 2 nb bytes (record layout), tested by logical_from_columns; optional iteration
+// sums (iters [B][2]) into counters[8], counters[9].
 // One wave per sample; counters as statistics_kernel (DecoderCPU.h:464-521).
 constexpr int kMaxRecWords = 80;  // 2 nb <= 640 bytes
 
 __global__ __launch_bounds__(64 * kStatWaves) void statistics_packed_kernel(
     const uint8_t* __restrict__ errp, const uint8_t* __restrict__ rec, const int32_t* __restrict__ iters, long long B,
-    int nb, const uint64_t* __restrict__ imp_rows, int imp_nrows, int imp_words, unsigned long long* __restrict__ counters)
+    int n, int nb, const uint64_t* __restrict__ imp_cols, int imp_cw, unsigned long long* __restrict__ counters)
 {
     __shared__ unsigned long long part[C_N + 2];
     __shared__ __attribute__((aligned(8))) uint8_t sres[kStatWaves][8 * kMaxRecWords];
@@ -358,8 +376,9 @@ __global__ __launch_bounds__(64 * kStatWaves) void statistics_packed_kernel(
     const bool live = b < B;
     const int recB = 2 * nb + 1;
     bool anyX = false, anyZ = false;
+    const int nw = (2 * nb + 7) / 8;
     if (live) {
-        for (int t = lane; t < 8 * imp_words; t += 64) {
+        for (int t = lane; t < 8 * nw; t += 64) {
             uint8_t r = 0;
             if (t < 2 * nb) {
                 const uint8_t e = errp[b * 2 * nb + t];
@@ -375,17 +394,9 @@ __global__ __launch_bounds__(64 * kStatWaves) void statistics_packed_kernel(
         const bool wx = __any(anyX), wz = __any(anyZ);
         const bool dEX = f & QEC_SYNDROME_FAIL_X, dEZ = f & QEC_SYNDROME_FAIL_Z;
         bool logical = false;
-        if (!(dEX || dEZ) && imp_nrows > 0) {  // CheckLogicalError only when no syndrome failure
-            const uint64_t* res = reinterpret_cast<const uint64_t*>(sres[wv]);
-            bool odd = false;
-            for (int row = lane; row < imp_nrows; row += 64) {
-                const uint64_t* rp = imp_rows + (size_t)row * imp_words;
-                unsigned long long acc = 0;
-                for (int w = 0; w < imp_words; ++w) acc ^= rp[w] & res[w];
-                odd |= (__popcll(acc) & 1) != 0;
-            }
-            logical = __any(odd);
-        }
+        if (!(dEX || dEZ) && imp_cw > 0)  // CheckLogicalError only when no syndrome failure
+            logical = logical_from_columns<true>(reinterpret_cast<const unsigned long long*>(sres[wv]), nw, n, nb,
+                                                 imp_cols, imp_cw, lane);
         if (lane == 0) {
             atomicAdd(&part[C_WITHX], (unsigned long long)wx);
             atomicAdd(&part[C_WITHZ], (unsigned long long)wz);
@@ -444,7 +455,7 @@ int launch_mc_errors_syndrome(int src, const McArgsHost& h, hipStream_t st)
     const int npad = 8 * a.nb;
     a.S = (a.chkVar == nullptr && c.P > 0 && c.P < 64) ? 64 / c.P : 1;
     if ((size_t)a.S * 2 * npad > 4096) a.S = 1;
-    auto magic = [](long long d) { return d > 0 ? (uint32_t)(((1ull << 32) + (uint64_t)d - 1) / (uint64_t)d) : 0u; };
+    auto magic = [](long long d) { return d > 1 ? (uint32_t)(((1ull << 32) + (uint64_t)d - 1) / (uint64_t)d) : 0u; };
     a.magicW = magic(h.W); a.magicG = magic(npad / 4); a.magicN = magic(npad); a.magicM = magic(c.mX + c.mZ);
     a.magicP = magic(c.P); a.magicB = magic(2 * a.nb);
     if ((long long)a.S * std::max<long long>({(long long)h.W, npad, (long long)c.mX + c.mZ}) >= 65536)
@@ -462,25 +473,25 @@ int launch_mc_errors_syndrome(int src, const McArgsHost& h, hipStream_t st)
     return launch_check("mc_errors_syndrome");
 }
 
-int launch_statistics_packed(const Code& c, const uint64_t* imp_rec_dev, const uint8_t* errp, const uint8_t* rec,
+int launch_statistics_packed(const Code& c, const uint64_t* imp_cols, const uint8_t* errp, const uint8_t* rec,
                              const int32_t* iters, long long B, unsigned long long* counters, hipStream_t st)
 {
     if (B <= 0) return QEC_OK;
-    if (c.imp_words_rec > kMaxRecWords) return fail(QEC_ERR_UNSUPPORTED, "packed statistics kernel: 2 ceil(n/8) > 640");
-    const int nrows = c.imp_words_rec ? (int)(c.imp_rows_rec.size() / c.imp_words_rec) : 0;
+    const int nb = (c.n + 7) / 8;
+    if ((2 * nb + 7) / 8 > kMaxRecWords || c.imp_col_words > 64)
+        return fail(QEC_ERR_UNSUPPORTED, "packed statistics kernel: code too long");
     hipLaunchKernelGGL(statistics_packed_kernel, dim3((unsigned)((B + kStatWaves - 1) / kStatWaves)), dim3(64 * kStatWaves),
-                       0, st, errp, rec, iters, B, (c.n + 7) / 8, imp_rec_dev, nrows, c.imp_words_rec, counters);
+                       0, st, errp, rec, iters, B, c.n, nb, imp_cols, c.imp_col_words, counters);
     return launch_check("statistics_packed");
 }
 
-int launch_statistics(const Code& c, const uint64_t* imp_dev, const uint8_t* x, const uint8_t* z, const uint8_t* eX,
+int launch_statistics(const Code& c, const uint64_t* imp_cols, const uint8_t* x, const uint8_t* z, const uint8_t* eX,
                       const uint8_t* eZ, const uint8_t* flags, long long B, unsigned long long* counters, hipStream_t st)
 {
     if (B <= 0) return QEC_OK;
-    if (2 * c.n > 64 * kMaxWords) return fail(QEC_ERR_UNSUPPORTED, "statistics kernel: 2n > 4096");
-    const int nrows = c.imp_words ? (int)(c.imp_rows.size() / c.imp_words) : 0;
+    if (2 * c.n > 64 * kMaxWords || c.imp_col_words > 64) return fail(QEC_ERR_UNSUPPORTED, "statistics kernel: 2n > 4096");
     hipLaunchKernelGGL(statistics_kernel, dim3((unsigned)((B + kStatWaves - 1) / kStatWaves)), dim3(64 * kStatWaves), 0, st,
-                       x, z, eX, eZ, flags, B, c.n, imp_dev, nrows, c.imp_words, counters);
+                       x, z, eX, eZ, flags, B, c.n, imp_cols, c.imp_col_words, counters);
     return launch_check("statistics");
 }
 

@@ -29,10 +29,10 @@ struct Code {
     // Bit-packed I-P rows that are not all-zero (for CheckLogicalError).
     int imp_words = 0;                 // u64 words per packed 2n-bit row
     std::vector<uint64_t> imp_rows;    // nnz_rows x imp_words
-    // The same rows in the decision-record layout (qec_decode_batch_packed_dev): x qubit q at bit q,
-    // z qubit t at bit 8 ceil(n/8) + t.
-    int imp_words_rec = 0;
-    std::vector<uint64_t> imp_rows_rec;
+    // Columns of I-P over its non-zero rows (2n x imp_col_words, bit k = k-th non-zero row): the
+    // device statistics kernels XOR the columns at the residual's set bits.
+    int imp_col_words = 0;
+    std::vector<uint64_t> imp_cols;
     std::string describe() const;      // operator<< of Quantum_LDPC_Code.h:145-150
 };
 

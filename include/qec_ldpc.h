@@ -68,7 +68,8 @@ enum { QEC_SECTOR_X = 0, QEC_SECTOR_Z = 1 };
 enum {
     QEC_ENGINE_AUTO = 0,       /* wave-circulant if the code has an instantiated kernel, else sparse-graph */
     QEC_ENGINE_CIRCULANT = 1,  /* wave-circulant: circulant-permutation QC codes, P <= 64 (bp_decode.hip) */
-    QEC_ENGINE_SPARSE = 2      /* sparse-graph: any code DecoderCPU accepts (regular, dc = L, dv = J / K) */
+    QEC_ENGINE_SPARSE = 2,     /* sparse-graph: any code DecoderCPU accepts (regular, dc = L, dv = J / K) */
+    QEC_ENGINE_CPU = 3         /* host threads, device -1 (DecoderCPU's drop-in; cpu_engine.cpp) */
 };
 
 typedef struct qec_code qec_code;
@@ -119,8 +120,11 @@ int qec_code_syndrome(const qec_code* code, int sector, const uint8_t* e, size_t
 int qec_code_check_logical(const qec_code* code, const uint8_t* ex, const uint8_t* ez, size_t B, uint8_t* out);
 
 /* ---- decoder (DecoderGPU, QEC_LDPC/DecoderGPU.h:11-281) ------------------- */
-/* Replaces DecoderGPU(Quantum_LDPC_Code) (DecoderGPU.h:117-130).  device = HIP
- * device ordinal (>= 0; there is no CPU engine in the product).  max_batch sizes the
+/* Replaces DecoderGPU(Quantum_LDPC_Code) (DecoderGPU.h:117-130) and, with device = -1,
+ * DecoderCPU(Quantum_LDPC_Code) (DecoderCPU.h:16-39): the CPU engine, host threads over
+ * edge-major tables, bit-identical decisions; it serves the host-buffer entry points and
+ * qec_get_statistics (the _dev entry points and qec_monte_carlo need a GPU and fail with
+ * QEC_ERR_UNSUPPORTED).  device >= 0 = HIP device ordinal.  max_batch sizes the
  * device-pointer workspace up front: the _dev decode entry points then allocate nothing
  * for B <= max_batch and may be captured into a graph.  Larger batches grow it on
  * demand (an error while the stream is being captured). */

@@ -25,7 +25,7 @@ SYNDROME_FAIL_Z = 2
 CONVERGENCE_FAIL_X = 4
 CONVERGENCE_FAIL_Z = 8
 STOP = {"ref": 0, "fixed": 1, "syndrome": 2}
-ENGINE = {"auto": 0, "circulant": 1, "sparse": 2}
+ENGINE = {"auto": 0, "circulant": 1, "sparse": 2, "cpu": 3}
 OPTION = {"hard_paths": 1, "cycle_jump": 2, "schedule": 3, "sector_split": 4, "phase_stats": 5}
 
 # every symbol include/qec_ldpc.h declares
@@ -516,6 +516,20 @@ class DecoderGPU:
         _check(lib().qec_get_statistics(self._h, errorWeight, numErrors, float(errorProbability), maxIterations,
                                         seed & 0xFFFFFFFF, nThreads, ctypes.byref(st)), "qec_get_statistics")
         return st.as_dict()
+
+
+class DecoderCPU(DecoderGPU):
+    """The reference's DecoderCPU slot (QEC_LDPC/DecoderCPU.h): the library's CPU engine
+    (device -1; host threads, bit-identical decisions).  Host-buffer entry points and
+    GetStatistics only."""
+
+    def __init__(self, code):
+        super().__init__(code, device=-1, engine="cpu")
+
+    def GetStatistics(self, errorWeight, numErrors, errorProbability, maxIterations, seed=None, nThreads=None):
+        # the reference tests (numErrors / threads) * threads samples with its OpenMP thread count
+        return super().GetStatistics(errorWeight, numErrors, errorProbability, maxIterations, seed,
+                                     nThreads if nThreads is not None else 1)
 
 
 def format_statistics(code, st):

@@ -37,6 +37,11 @@ const int32_t* sparse_plan_chkvar(const void* plan);
 int launch_decode_sparse(void* plan, const uint8_t* sX, const uint8_t* sZ, long long B, float errorProbability,
                          int maxIter, int stop, uint8_t* eX, uint8_t* eZ, uint8_t* flags, int32_t* iters, float* q,
                          hipStream_t stream);
+void* cpu_plan_create(const Code& c);
+void cpu_plan_free(void* plan);
+int cpu_threads();
+int cpu_decode_batch(void* plan, const uint8_t* sX, const uint8_t* sZ, long long B, float p, int maxIter, int stop,
+                     uint8_t* eX, uint8_t* eZ, uint8_t* flags, uint8_t* rec, int32_t* iters, float* qf, int threads);
 int launch_pack_decisions(const uint8_t* eX, const uint8_t* eZ, const uint8_t* flags, long long B, int n, uint8_t* out,
                           hipStream_t st);
 int launch_statistics(const Code& c, const uint64_t* imp_cols, const uint8_t* x, const uint8_t* z, const uint8_t* eX,
@@ -58,6 +63,7 @@ struct qec_decoder {
     int engine = QEC_ENGINE_CIRCULANT;
     const void* variant = nullptr;  // wave-circulant kernel variant (bp_decode.hip)
     void* sparse = nullptr;         // sparse-graph plan (bp_sparse.hip)
+    void* cpu = nullptr;            // CPU engine plan (cpu_engine.cpp), device = -1
     std::string variant_name;
     int hard_paths = 1;             // QEC_OPT_HARD_PATHS
     int cycle_jump = 1;             // QEC_OPT_CYCLE_JUMP
@@ -88,7 +94,8 @@ struct qec_decoder {
     ~qec_decoder()
     {
         for (qec_decoder* p : parts) delete p;
-        if (parts.empty()) {
+        if (cpu) cpu_plan_free(cpu);
+        if (parts.empty() && !cpu) {
             (void)hipSetDevice(device);
             if (ws_ev) (void)hipEventDestroy(ws_ev);
             if (stream) (void)hipStreamDestroy(stream);
@@ -264,10 +271,24 @@ qec_decoder* qec_decoder_create(const qec_code* h, int device, size_t max_batch)
 qec_decoder* qec_decoder_create_engine(const qec_code* h, int device, size_t max_batch, int engine)
 {
     if (!h) { fail(QEC_ERR_ARG, "qec_decoder_create: null code"); return nullptr; }
-    if (device < 0) { fail(QEC_ERR_ARG, "qec_decoder_create: the product has no CPU engine; device must be >= 0"); return nullptr; }
-    if (engine < QEC_ENGINE_AUTO || engine > QEC_ENGINE_SPARSE) {
+    if (engine < QEC_ENGINE_AUTO || engine > QEC_ENGINE_CPU) {
         fail(QEC_ERR_ARG, "qec_decoder_create_engine: unknown engine");
         return nullptr;
+    }
+    if (device < 0 || engine == QEC_ENGINE_CPU) {  // DecoderCPU: host buffers only
+        if (device >= 0 || (engine != QEC_ENGINE_AUTO && engine != QEC_ENGINE_CPU)) {
+            fail(QEC_ERR_ARG, "qec_decoder_create: the CPU engine is device -1, the GPU engines devices >= 0");
+            return nullptr;
+        }
+        std::unique_ptr<qec_decoder> d(new (std::nothrow) qec_decoder);
+        if (!d) { fail(QEC_ERR_NOMEM, "qec_decoder_create: out of memory"); return nullptr; }
+        d->code = std::make_shared<const Code>(h->c);
+        d->device = -1;
+        d->engine = QEC_ENGINE_CPU;
+        d->cpu = cpu_plan_create(*d->code);
+        if (!d->cpu) return nullptr;
+        d->variant_name = "cpu (" + std::to_string(cpu_threads()) + " threads) " + d->code->describe();
+        return d.release();
     }
     std::string name;
     const void* v = engine == QEC_ENGINE_SPARSE ? nullptr : select_variant(h->c, name);
@@ -495,6 +516,7 @@ int check_decode_args(const qec_decoder* d, const void* sX, const void* sZ, size
 
 int single_device_only(const qec_decoder* d, const char* what)
 {
+    if (d->cpu) return fail(QEC_ERR_UNSUPPORTED, std::string(what) + ": the CPU engine has no device buffers");
     if (!d->parts.empty())
         return fail(QEC_ERR_ARG, std::string(what) + ": device buffers live on one GPU; call it on a part "
                                                      "(qec_decoder_part) of a multi-device decoder");
@@ -506,6 +528,7 @@ int decode_host(qec_decoder* d, const uint8_t* sX, const uint8_t* sZ, size_t B, 
                 uint8_t* eX, uint8_t* eZ, uint8_t* flags, uint8_t* rec, int32_t* iters, float* q)
 {
     if (B == 0) return QEC_OK;
+    if (d->cpu) return cpu_decode_batch(d->cpu, sX, sZ, (long long)B, p, maxIter, stop, eX, eZ, flags, rec, iters, q, 0);
     QEC_DEVICE_SCOPE(d->device);
     const Code& c = *d->code;
     const size_t qn = (size_t)(c.mX + c.mZ) * c.L;
@@ -730,6 +753,75 @@ int monte_carlo_part(qec_decoder* d, uint64_t seed, uint64_t start, uint64_t cou
     return QEC_OK;
 }
 
+// GetStatistics on the CPU engine: the same draws, host syndromes, CPU decode (reference stop
+// rule), host counting (DecoderCPU.h:448-521).
+int cpu_statistics(qec_decoder* d, int W, long tested, float p, int maxIter, uint32_t seed, qec_stats* out)
+{
+    const Code& c = *d->code;
+    const int n = c.n;
+    const long CH = 1 << 14;
+    std::vector<uint8_t> x, z, sx, sz, ex, ez, fl, rx(n), rz(n);
+    unsigned long long cn[QEC_MC_NCOUNTERS] = {};
+    Mt19937 g(seed);
+    for (long base = 0; base < tested; base += CH) {
+        const long cnt = std::min(CH, tested - base);
+        x.assign((size_t)cnt * n, 0);
+        z.assign((size_t)cnt * n, 0);
+        for (long s = 0; s < cnt; ++s)
+            for (int w = 0; w < W; ++w) {
+                const uint32_t v = g.msvc_uniform((uint32_t)n), t = g.msvc_uniform(3u);  // DecoderCPU.h:452-457
+                if (t == 0 || t == 1) x[(size_t)s * n + v] = 1;
+                if (t == 2 || t == 1) z[(size_t)s * n + v] = 1;
+            }
+        sx.resize((size_t)cnt * c.mX);
+        sz.resize((size_t)cnt * c.mZ);
+        for (long s = 0; s < cnt; ++s) {
+            host_syndrome(c, 0, &x[(size_t)s * n], &sx[(size_t)s * c.mX]);
+            host_syndrome(c, 1, &z[(size_t)s * n], &sz[(size_t)s * c.mZ]);
+        }
+        ex.resize((size_t)cnt * n);
+        ez.resize((size_t)cnt * n);
+        fl.resize(cnt);
+        const int rc = cpu_decode_batch(d->cpu, sx.data(), sz.data(), cnt, p, maxIter, QEC_STOP_REF, ex.data(), ez.data(),
+                                        fl.data(), nullptr, nullptr, nullptr, 0);
+        if (rc) return rc;
+        for (long s = 0; s < cnt; ++s) {
+            bool ax = false, az = false;
+            for (int v = 0; v < n; ++v) {
+                ax |= x[(size_t)s * n + v] != 0;
+                az |= z[(size_t)s * n + v] != 0;
+            }
+            cn[QEC_MC_WITHX] += ax;
+            cn[QEC_MC_WITHZ] += az;
+            const bool dEX = fl[s] & QEC_SYNDROME_FAIL_X, dEZ = fl[s] & QEC_SYNDROME_FAIL_Z;
+            cn[QEC_MC_SYNX] += dEX;
+            cn[QEC_MC_SYNZ] += dEZ;
+            if (!(dEX || dEZ)) {
+                for (int v = 0; v < n; ++v) {
+                    rx[v] = x[(size_t)s * n + v] ^ ex[(size_t)s * n + v];
+                    rz[v] = z[(size_t)s * n + v] ^ ez[(size_t)s * n + v];
+                }
+                ++cn[host_check_logical(c, rx.data(), rz.data()) ? QEC_MC_LOGICAL : QEC_MC_CORRECTED];
+            }
+            cn[QEC_MC_CONVX] += (fl[s] & QEC_CONVERGENCE_FAIL_X) != 0;
+            cn[QEC_MC_CONVZ] += (fl[s] & QEC_CONVERGENCE_FAIL_Z) != 0;
+        }
+    }
+    std::memset(out, 0, sizeof *out);
+    out->randSeed = seed;
+    out->numErrorsTested = (uint32_t)tested;
+    out->numXErrorsTested = (uint32_t)cn[QEC_MC_WITHX];
+    out->numZErrorsTested = (uint32_t)cn[QEC_MC_WITHZ];
+    out->errorWeight = (uint32_t)W;
+    out->corrected = (uint32_t)cn[QEC_MC_CORRECTED];
+    out->syndromeErrorsX = (uint32_t)cn[QEC_MC_SYNX];
+    out->syndromeErrorsZ = (uint32_t)cn[QEC_MC_SYNZ];
+    out->logicalErrors = (uint32_t)cn[QEC_MC_LOGICAL];
+    out->convergenceFailX = (uint32_t)cn[QEC_MC_CONVX];
+    out->convergenceFailZ = (uint32_t)cn[QEC_MC_CONVZ];
+    return QEC_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -750,6 +842,12 @@ int qec_get_statistics(qec_decoder* d, int W, int numErrors, float p, int maxIte
     if (nThreads < 1) nThreads = 1;
     const auto t0 = std::chrono::high_resolution_clock::now();
     const long tested = (long)(numErrors / nThreads) * nThreads;  // DecoderCPU.h:426,527
+    if (d->cpu) {
+        const int rc = cpu_statistics(d, W, tested, p, maxIter, seed, out);
+        out->durationMicroSeconds = std::chrono::duration_cast<std::chrono::microseconds>(
+                                        std::chrono::high_resolution_clock::now() - t0).count();
+        return rc;
+    }
     const long CH = 1 << 16;
     const int n = c.n;
     const std::vector<qec_decoder*> parts = parts_of(d);
@@ -834,6 +932,7 @@ int qec_monte_carlo(qec_decoder* d, uint64_t seed, uint64_t start, uint64_t coun
                     size_t batch, qec_mc_result* out)
 {
     if (!d || !out || (stop < QEC_STOP_REF || stop > QEC_STOP_SYNDROME)) return fail(QEC_ERR_ARG, "qec_monte_carlo: bad argument");
+    if (d->cpu) return fail(QEC_ERR_UNSUPPORTED, "qec_monte_carlo: a device pipeline; the CPU engine has GetStatistics");
     const Code& c = *d->code;
     if (c.imp.empty()) return fail(QEC_ERR_UNSUPPORTED, "qec_monte_carlo: code has no I-P matrix for the logical check");
     if (batch == 0) batch = 65536;

@@ -117,7 +117,6 @@ enum { C_WITHX, C_WITHZ, C_SYNX, C_SYNZ, C_LOGICAL, C_CORRECTED, C_CONVX, C_CONV
 // reads a few columns instead of every row (P61: 678 x 20 words per sample).  res[0..nw) is the
 // residual in LDS, the same for every lane; REC: record layout (x bits at [0, 8 nb), z bits at
 // [8 nb, 16 nb)), else qubit layout (bit q = qubit q of [x | z]).
-constexpr int kStatWaves = 4;
 constexpr int kMaxWords = 64;  // 2n <= 4096 qubits
 
 template <bool REC>
@@ -140,23 +139,44 @@ __device__ __forceinline__ bool logical_from_columns(const unsigned long long* r
     return __any(acc != 0);
 }
 
-// One wave per sample.  Residual words are formed with ballots (lane = qubit within a
-// 64-qubit word) and parked in LDS for the column test above.
+// Grid-stride over samples, one wave per sample at a time; each wave keeps its counts in
+// registers and the workgroup adds them to `counters` once (same-address atomics from every
+// workgroup serialise at L2: 16 384 four-wave workgroups x 8 counters cost ~190 us per 65 536
+// samples, profiles/r02/mc_r02f_trace.csv).
+constexpr int kStatBlockWaves = 16;
+constexpr int kStatMaxBlocks = 512;
 
-__global__ __launch_bounds__(64 * kStatWaves) void statistics_kernel(
+__device__ __forceinline__ void stat_flush(unsigned long long (*part)[C_N + 2], const unsigned long long* c, int nc,
+                                           unsigned long long* __restrict__ counters)
+{
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    if (lane < nc) {
+        unsigned long long v = 0;
+        for (int k = 0; k < C_N + 2; ++k) v = lane == k ? c[k] : v;
+        part[wv][lane] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < nc) {
+        unsigned long long v = 0;
+        for (int w = 0; w < kStatBlockWaves; ++w) v += part[w][threadIdx.x];
+        if (v) atomicAdd(&counters[threadIdx.x], v);
+    }
+}
+
+// Residual words are formed with ballots (lane = qubit within a 64-qubit word) and parked in LDS
+// for the column test above.
+__global__ __launch_bounds__(64 * kStatBlockWaves) void statistics_kernel(
     const uint8_t* __restrict__ x, const uint8_t* __restrict__ z, const uint8_t* __restrict__ eX,
     const uint8_t* __restrict__ eZ, const uint8_t* __restrict__ flags, long long B, int n,
     const uint64_t* __restrict__ imp_cols, int imp_cw, unsigned long long* __restrict__ counters)
 {
-    __shared__ unsigned long long part[C_N];
-    __shared__ unsigned long long sres[kStatWaves][kMaxWords];
-    if (threadIdx.x < C_N) part[threadIdx.x] = 0;
+    __shared__ unsigned long long part[kStatBlockWaves][C_N + 2];
+    __shared__ unsigned long long sres[kStatBlockWaves][kMaxWords];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const long long b = (long long)blockIdx.x * kStatWaves + wv;
-    const bool live = b < B;
     const int nw = (2 * n + 63) / 64;
-    bool anyX = false, anyZ = false;
-    if (live) {
+    unsigned long long c[C_N + 2] = {};
+    for (long long b = (long long)blockIdx.x * kStatBlockWaves + wv; b < B; b += (long long)gridDim.x * kStatBlockWaves) {
+        bool anyX = false, anyZ = false;
         for (int w = 0; w < nw; ++w) {
             const int q = w * 64 + lane;
             bool bit = false;
@@ -172,27 +192,23 @@ __global__ __launch_bounds__(64 * kStatWaves) void statistics_kernel(
             const unsigned long long word = __ballot(bit);
             if (lane == 0) sres[wv][w] = word;
         }
-    }
-    __syncthreads();
-    if (live) {
+        wave_sync();
         const uint8_t f = flags[b];
-        const bool wx = __any(anyX), wz = __any(anyZ);
         const bool dEX = f & QEC_SYNDROME_FAIL_X, dEZ = f & QEC_SYNDROME_FAIL_Z;
         bool logical = false;
         if (!(dEX || dEZ) && imp_cw > 0)  // CheckLogicalError only when no syndrome failure
             logical = logical_from_columns<false>(sres[wv], nw, n, 0, imp_cols, imp_cw, lane);
-        if (lane == 0) {
-            atomicAdd(&part[C_WITHX], (unsigned long long)wx);
-            atomicAdd(&part[C_WITHZ], (unsigned long long)wz);
-            atomicAdd(&part[C_SYNX], (unsigned long long)dEX);
-            atomicAdd(&part[C_SYNZ], (unsigned long long)dEZ);
-            if (!(dEX || dEZ)) atomicAdd(&part[logical ? C_LOGICAL : C_CORRECTED], 1ull);
-            atomicAdd(&part[C_CONVX], (unsigned long long)((f & QEC_CONVERGENCE_FAIL_X) != 0));
-            atomicAdd(&part[C_CONVZ], (unsigned long long)((f & QEC_CONVERGENCE_FAIL_Z) != 0));
-        }
+        wave_sync();  // sres is rewritten by the next sample
+        c[C_WITHX] += __any(anyX);
+        c[C_WITHZ] += __any(anyZ);
+        c[C_SYNX] += dEX;
+        c[C_SYNZ] += dEZ;
+        c[C_LOGICAL] += !(dEX || dEZ) && logical;
+        c[C_CORRECTED] += !(dEX || dEZ) && !logical;
+        c[C_CONVX] += (f & QEC_CONVERGENCE_FAIL_X) != 0;
+        c[C_CONVZ] += (f & QEC_CONVERGENCE_FAIL_Z) != 0;
     }
-    __syncthreads();
-    if (threadIdx.x < C_N && part[threadIdx.x]) atomicAdd(&counters[threadIdx.x], part[threadIdx.x]);
+    stat_flush(part, c, C_N, counters);
 }
 
 // Decision records for the cross-rank gather: per syndrome, eX bit-packed
@@ -257,7 +273,9 @@ __device__ __forceinline__ int qdiv(int t, uint32_t magic) { return magic ? (int
 
 // A wave handles S = max(1, floor(64 / P)) samples (P61: 1, P7: 9), so short codes keep the lanes
 // busy; each phase spreads its (sample, item) pairs over the lanes.
-template <int SRC>
+// LT: the block-column count L when known at compile time (the shipped codes: 10 and 6), so the
+// syndrome's L-term XOR is unrolled with every LDS read in flight at once; 0 = a.L at run time.
+template <int SRC, int LT>
 __global__ __launch_bounds__(64 * kMcWaves) void mc_errors_syndrome_kernel(const McArgs a)
 {
     extern __shared__ __attribute__((aligned(8))) uint8_t mc_smem[];
@@ -285,6 +303,7 @@ __global__ __launch_bounds__(64 * kMcWaves) void mc_errors_syndrome_kernel(const
         // four qubits per lane and Philox call, one 32-bit LDS word per row (npad is a multiple of
         // 8, so the padding words are written too, zero past n)
         const int ng = npad / 4;
+#pragma unroll 3
         for (int t = lane; t < ns * ng; t += 64) {
             const int sI = qdiv(t, a.magicG), g = t - sI * ng;
             uint32_t x4 = 0, z4 = 0;
@@ -327,7 +346,7 @@ __global__ __launch_bounds__(64 * kMcWaves) void mc_errors_syndrome_kernel(const
             if (zs) a.sZ[b * a.mZ + (c - a.mX)] = (uint8_t)(x & 1u); else a.sX[b * a.mX + c] = (uint8_t)(x & 1u);
         }
     } else {  // QC: lane (sample, i) computes checks (r, i) of every block row; E[r][l] is uniform
-        const int P = a.P, L = a.L;
+        const int P = a.P, L = LT > 0 ? LT : a.L;
         for (int t = lane; t < ns * P; t += 64) {
             const int sI = qdiv(t, a.magicP), i = t - sI * P;
             const long long b = b0 + sI;
@@ -337,10 +356,17 @@ __global__ __launch_bounds__(64 * kMcWaves) void mc_errors_syndrome_kernel(const
                 const uint8_t* e = zs ? ex + npad : ex;
                 const int* E = zs ? a.EZ + (r - a.J) * L : a.EX + r * L;
                 uint32_t x = 0;
-                for (int l = 0; l < L; ++l) {
-                    int j = E[l] + i;
-                    j -= (j >= P) ? P : 0;
-                    x ^= e[l * P + j];
+                if constexpr (LT > 0) {
+#pragma unroll
+                    for (int l = 0; l < LT; ++l) {
+                        const uint32_t j = (uint32_t)(E[l] + i);
+                        x ^= e[l * P + min(j, j - (uint32_t)P)];  // (E + i) mod P: j - P wraps above j when j < P
+                    }
+                } else {
+                    for (int l = 0; l < L; ++l) {
+                        const uint32_t j = (uint32_t)(E[l] + i);
+                        x ^= e[l * P + min(j, j - (uint32_t)P)];
+                    }
                 }
                 if (zs) a.sZ[b * a.mZ + (r - a.J) * P + i] = (uint8_t)(x & 1u);
                 else a.sX[b * a.mX + r * P + i] = (uint8_t)(x & 1u);
@@ -364,20 +390,18 @@ __global__ __launch_bounds__(64 * kMcWaves) void mc_errors_syndrome_kernel(const
 // One wave per sample; counters as statistics_kernel (DecoderCPU.h:464-521).
 constexpr int kMaxRecWords = 80;  // 2 nb <= 640 bytes
 
-__global__ __launch_bounds__(64 * kStatWaves) void statistics_packed_kernel(
+__global__ __launch_bounds__(64 * kStatBlockWaves) void statistics_packed_kernel(
     const uint8_t* __restrict__ errp, const uint8_t* __restrict__ rec, const int32_t* __restrict__ iters, long long B,
     int n, int nb, const uint64_t* __restrict__ imp_cols, int imp_cw, unsigned long long* __restrict__ counters)
 {
-    __shared__ unsigned long long part[C_N + 2];
-    __shared__ __attribute__((aligned(8))) uint8_t sres[kStatWaves][8 * kMaxRecWords];
-    if (threadIdx.x < C_N + 2) part[threadIdx.x] = 0;
+    __shared__ unsigned long long part[kStatBlockWaves][C_N + 2];
+    __shared__ __attribute__((aligned(8))) uint8_t sres[kStatBlockWaves][8 * kMaxRecWords];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const long long b = (long long)blockIdx.x * kStatWaves + wv;
-    const bool live = b < B;
     const int recB = 2 * nb + 1;
-    bool anyX = false, anyZ = false;
     const int nw = (2 * nb + 7) / 8;
-    if (live) {
+    unsigned long long c[C_N + 2] = {};
+    for (long long b = (long long)blockIdx.x * kStatBlockWaves + wv; b < B; b += (long long)gridDim.x * kStatBlockWaves) {
+        bool anyX = false, anyZ = false;
         for (int t = lane; t < 8 * nw; t += 64) {
             uint8_t r = 0;
             if (t < 2 * nb) {
@@ -387,33 +411,28 @@ __global__ __launch_bounds__(64 * kStatWaves) void statistics_packed_kernel(
             }
             sres[wv][t] = r;
         }
-    }
-    __syncthreads();
-    if (live) {
+        wave_sync();
         const uint8_t f = rec[b * recB + 2 * nb];
-        const bool wx = __any(anyX), wz = __any(anyZ);
         const bool dEX = f & QEC_SYNDROME_FAIL_X, dEZ = f & QEC_SYNDROME_FAIL_Z;
         bool logical = false;
         if (!(dEX || dEZ) && imp_cw > 0)  // CheckLogicalError only when no syndrome failure
             logical = logical_from_columns<true>(reinterpret_cast<const unsigned long long*>(sres[wv]), nw, n, nb,
                                                  imp_cols, imp_cw, lane);
-        if (lane == 0) {
-            atomicAdd(&part[C_WITHX], (unsigned long long)wx);
-            atomicAdd(&part[C_WITHZ], (unsigned long long)wz);
-            atomicAdd(&part[C_SYNX], (unsigned long long)dEX);
-            atomicAdd(&part[C_SYNZ], (unsigned long long)dEZ);
-            if (!(dEX || dEZ)) atomicAdd(&part[logical ? C_LOGICAL : C_CORRECTED], 1ull);
-            atomicAdd(&part[C_CONVX], (unsigned long long)((f & QEC_CONVERGENCE_FAIL_X) != 0));
-            atomicAdd(&part[C_CONVZ], (unsigned long long)((f & QEC_CONVERGENCE_FAIL_Z) != 0));
-            if (iters != nullptr) {
-                atomicAdd(&part[C_N], (unsigned long long)iters[2 * b]);
-                atomicAdd(&part[C_N + 1], (unsigned long long)iters[2 * b + 1]);
-            }
+        wave_sync();
+        c[C_WITHX] += __any(anyX);
+        c[C_WITHZ] += __any(anyZ);
+        c[C_SYNX] += dEX;
+        c[C_SYNZ] += dEZ;
+        c[C_LOGICAL] += !(dEX || dEZ) && logical;
+        c[C_CORRECTED] += !(dEX || dEZ) && !logical;
+        c[C_CONVX] += (f & QEC_CONVERGENCE_FAIL_X) != 0;
+        c[C_CONVZ] += (f & QEC_CONVERGENCE_FAIL_Z) != 0;
+        if (iters != nullptr) {
+            c[C_N] += (unsigned)iters[2 * b];
+            c[C_N + 1] += (unsigned)iters[2 * b + 1];
         }
     }
-    __syncthreads();
-    const int nc = iters != nullptr ? C_N + 2 : C_N;
-    if (threadIdx.x < nc && part[threadIdx.x]) atomicAdd(&counters[threadIdx.x], part[threadIdx.x]);
+    stat_flush(part, c, iters != nullptr ? C_N + 2 : C_N, counters);
 }
 
 // ---- launchers --------------------------------------------------------------
@@ -464,12 +483,18 @@ int launch_mc_errors_syndrome(int src, const McArgsHost& h, hipStream_t st)
     if (smem > 64 * 1024) return fail(QEC_ERR_UNSUPPORTED, "mc front end: code too long for the LDS stage");
     const long long per_block = (long long)kMcWaves * a.S;
     const dim3 grid((unsigned)((h.B + per_block - 1) / per_block)), block(64 * kMcWaves);
+    auto launch = [&](auto kern) { hipLaunchKernelGGL(kern, grid, block, smem, st, a); };
+    const int lt = a.chkVar == nullptr && (c.L == 10 || c.L == 6) ? c.L : 0;
+#define QEC_MC_LAUNCH(S)                                                              \
+    (lt == 10 ? launch(mc_errors_syndrome_kernel<S, 10>)                              \
+              : lt == 6 ? launch(mc_errors_syndrome_kernel<S, 6>) : launch(mc_errors_syndrome_kernel<S, 0>))
     if (src == MC_SRC_PHILOX)
-        hipLaunchKernelGGL(mc_errors_syndrome_kernel<MC_SRC_PHILOX>, grid, block, smem, st, a);
+        QEC_MC_LAUNCH(MC_SRC_PHILOX);
     else if (src == MC_SRC_DRAWS)
-        hipLaunchKernelGGL(mc_errors_syndrome_kernel<MC_SRC_DRAWS>, grid, block, smem, st, a);
+        QEC_MC_LAUNCH(MC_SRC_DRAWS);
     else
-        hipLaunchKernelGGL(mc_errors_syndrome_kernel<MC_SRC_BYTES>, grid, block, smem, st, a);
+        QEC_MC_LAUNCH(MC_SRC_BYTES);
+#undef QEC_MC_LAUNCH
     return launch_check("mc_errors_syndrome");
 }
 
@@ -480,8 +505,9 @@ int launch_statistics_packed(const Code& c, const uint64_t* imp_cols, const uint
     const int nb = (c.n + 7) / 8;
     if ((2 * nb + 7) / 8 > kMaxRecWords || c.imp_col_words > 64)
         return fail(QEC_ERR_UNSUPPORTED, "packed statistics kernel: code too long");
-    hipLaunchKernelGGL(statistics_packed_kernel, dim3((unsigned)((B + kStatWaves - 1) / kStatWaves)), dim3(64 * kStatWaves),
-                       0, st, errp, rec, iters, B, c.n, nb, imp_cols, c.imp_col_words, counters);
+    const long long blocks = std::min<long long>((B + kStatBlockWaves - 1) / kStatBlockWaves, kStatMaxBlocks);
+    hipLaunchKernelGGL(statistics_packed_kernel, dim3((unsigned)blocks), dim3(64 * kStatBlockWaves), 0, st, errp, rec,
+                       iters, B, c.n, nb, imp_cols, c.imp_col_words, counters);
     return launch_check("statistics_packed");
 }
 
@@ -490,8 +516,9 @@ int launch_statistics(const Code& c, const uint64_t* imp_cols, const uint8_t* x,
 {
     if (B <= 0) return QEC_OK;
     if (2 * c.n > 64 * kMaxWords || c.imp_col_words > 64) return fail(QEC_ERR_UNSUPPORTED, "statistics kernel: 2n > 4096");
-    hipLaunchKernelGGL(statistics_kernel, dim3((unsigned)((B + kStatWaves - 1) / kStatWaves)), dim3(64 * kStatWaves), 0, st,
-                       x, z, eX, eZ, flags, B, c.n, imp_cols, c.imp_col_words, counters);
+    const long long blocks = std::min<long long>((B + kStatBlockWaves - 1) / kStatBlockWaves, kStatMaxBlocks);
+    hipLaunchKernelGGL(statistics_kernel, dim3((unsigned)blocks), dim3(64 * kStatBlockWaves), 0, st, x, z, eX, eZ, flags, B,
+                       c.n, imp_cols, c.imp_col_words, counters);
     return launch_check("statistics");
 }
 

@@ -741,7 +741,7 @@ __device__ __forceinline__ bool lane_syndrome_ok(const BpArgs& a, uint32_t hdmas
 template <int R, int L, int SEC, int STOP, bool LAST, class SH, class TU>
 __device__ __forceinline__ bool iteration(const BpArgs& a, float (&msg)[R][L], uint32_t sbits, int n, Lane& ln,
                                           float pp, float one_minus_pp, bool& hard, bool& agreed, bool& vagree,
-                                          uint32_t& hrows)
+                                          uint32_t& hrows, uint32_t& hd_out)
 {
     const int P = SH::P(a);
     // launder the permute bases so their per-rotation selects are recomputed inside the
@@ -768,6 +768,7 @@ __device__ __forceinline__ bool iteration(const BpArgs& a, float (&msg)[R][L], u
     if constexpr (STOP == QEC_STOP_REF) {
         if (n % 10 == 0) return group_all_sh<SH>(lane_converged<R, L>(msg), ln, P);  // DecoderCPU.h:287-290
     } else if constexpr (STOP == QEC_STOP_SYNDROME) {
+        hd_out = hdmask;  // the hard decision of the new state (what the post-processing would compute)
         return group_all_sh<SH>(lane_syndrome_ok<R, L, SEC, SH>(a, hdmask, sbits, ln), ln, P);
     }
     return false;
@@ -808,7 +809,7 @@ __device__ __forceinline__ float table0_entry(float pp, int e)
 
 template <int R, int L, int SEC, int STOP, class SH>
 __device__ __forceinline__ bool iteration0(const BpArgs& a, float (&msg)[R][L], uint32_t sbits, const Lane& ln,
-                                           const float* __restrict__ tab)
+                                           const float* __restrict__ tab, uint32_t& hd_out)
 {
     const int P = SH::P(a);
     const int* et = SH::template table<SEC>(a);
@@ -838,6 +839,7 @@ __device__ __forceinline__ bool iteration0(const BpArgs& a, float (&msg)[R][L], 
     if constexpr (STOP == QEC_STOP_REF) {
         return group_all_sh<SH>(lane_converged<R, L>(msg), ln, P);  // n = 0: DecoderCPU.h:287-290
     } else if constexpr (STOP == QEC_STOP_SYNDROME) {
+        hd_out = hdmask;
         return group_all_sh<SH>(lane_syndrome_ok<R, L, SEC, SH>(a, hdmask, sbits, ln), ln, P);
     }
     return false;
@@ -962,9 +964,17 @@ __device__ __forceinline__ void decode_sector(const BpArgs& a, Lane& ln, uint32_
     bool agreed = false, vagree = false;
     uint32_t hrows = 0;  // QEC_ROW_HARD: rows of the current state whose every message is +0 or 1.0
     int ph_soft = 0, ph_hard = 0, ph_agree = 0, ph_jump = 0;  // QEC_PHASE_STATS
+    // syndrome stop rule: the hard decision of the last executed iteration and its syndrome test
+    // (hd_valid: the current state is that iteration's output, i.e. not reached by a cycle jump).
+    // The post-processing's hard decision is the same function of the same messages, and its
+    // syndrome test the same test, so they are reused (group-uniform).
+    uint32_t hd_last = 0;
+    bool syn_last = false, hd_valid = false;
     if (QEC_TABLE0 && N >= 2 && active) {  // iteration 0 by table (see iteration0)
         ++it;
-        if (iteration0<R, L, SEC, STOP, SH>(a, msg, sbits, ln, tab0)) active = false;
+        syn_last = iteration0<R, L, SEC, STOP, SH>(a, msg, sbits, ln, tab0, hd_last);
+        hd_valid = true;
+        if (syn_last) active = false;
         if constexpr (QEC_PHASE_STATS) ph_soft += 1;
         n = 1;
     }
@@ -977,9 +987,10 @@ __device__ __forceinline__ void decode_sector(const BpArgs& a, Lane& ln, uint32_
         if (active) {
             ++it;
             const bool was_hard = hard;
-            if (iteration<R, L, SEC, STOP, false, SH, TU>(a, msg, sbits, n, ln, pp, one_minus_pp, hard, agreed,
-                                                          vagree, hrows))
-                active = false;
+            syn_last = iteration<R, L, SEC, STOP, false, SH, TU>(a, msg, sbits, n, ln, pp, one_minus_pp, hard, agreed,
+                                                                 vagree, hrows, hd_last);
+            hd_valid = true;
+            if (syn_last) active = false;
             if constexpr (QEC_PHASE_STATS) { ph_soft += !was_hard; ph_hard += was_hard && !agreed; ph_agree += agreed; }
             if constexpr (TU::kSaturate) {
                 st_agreed = vagree;
@@ -991,6 +1002,7 @@ __device__ __forceinline__ void decode_sector(const BpArgs& a, Lane& ln, uint32_
                     it += last - n;
                     if constexpr (QEC_PHASE_STATS) ph_jump = last - n;
                     active = false;
+                    hd_valid = false;
                     n = N;  // skips the peeled last iteration too
                 }
                 in_agree = vagree;
@@ -1000,7 +1012,9 @@ __device__ __forceinline__ void decode_sector(const BpArgs& a, Lane& ln, uint32_
     if (n == N - 1 && active) {
         ++it;
         const bool was_hard = hard;
-        iteration<R, L, SEC, STOP, true, SH, TU>(a, msg, sbits, n, ln, pp, one_minus_pp, hard, agreed, vagree, hrows);
+        syn_last = iteration<R, L, SEC, STOP, true, SH, TU>(a, msg, sbits, n, ln, pp, one_minus_pp, hard, agreed, vagree,
+                                                            hrows, hd_last);
+        hd_valid = true;
         if constexpr (QEC_PHASE_STATS) { ph_soft += !was_hard; ph_hard += was_hard && !agreed; ph_agree += agreed; }
         st_agreed = vagree;
     }
@@ -1014,7 +1028,12 @@ __device__ __forceinline__ void decode_sector(const BpArgs& a, Lane& ln, uint32_
     const int* et = SH::template table<SEC>(a);
     bool conv, syn_ok;
     uint32_t hdmask = 0;  // e[v] of this lane's variables (l, (i + C[l]) mod P), bit l
-    if (TU::kSaturate && all_live(st_agreed, in_range)) {
+    if (STOP == QEC_STOP_SYNDROME && all_live(hd_valid, in_range)) {
+        // the last iteration's hard decision and syndrome test are the post-processing's
+        conv = group_all_sh<SH>(lane_converged<R, L>(msg), ln, P);
+        hdmask = hd_last;
+        syn_ok = syn_last;
+    } else if (TU::kSaturate && all_live(st_agreed, in_range)) {
         // Every live group's state is hard and each variable's R messages are equal: the hard
         // decision is the value on any one of its edges (row 0's, rotation S[0][l], 0 with the
         // relabelling), the syndrome of that decision on check (r, i) is the XOR of the check's

@@ -263,7 +263,7 @@ struct McArgs {
     long long B;
     int n, nb, L, P, J, K, mX, mZ;
     int S;                                     // samples per wave
-    uint32_t magicW, magicG, magicN, magicM, magicP, magicB;  // ceil(2^32 / d) for the item counts
+    uint32_t magicW, magicG, magicG2, magicN, magicM, magicP, magicB;  // ceil(2^32 / d) for the item counts
     int EX[128], EZ[128];
 };
 
@@ -345,31 +345,51 @@ __global__ __launch_bounds__(64 * kMcWaves) void mc_errors_syndrome_kernel(const
             const long long b = b0 + sI;
             if (zs) a.sZ[b * a.mZ + (c - a.mX)] = (uint8_t)(x & 1u); else a.sX[b * a.mX + c] = (uint8_t)(x & 1u);
         }
-    } else {  // QC: lane (sample, i) computes checks (r, i) of every block row; E[r][l] is uniform
+    } else {
+        // QC: the syndrome is the XOR of the H columns of the qubits in error, which are few (a
+        // depolarising sample at p = 0.01 hits ~6 of 610): each lane scans its words of the staged
+        // rows and, for every set byte, flips that qubit's R checks in an LDS bit set (ds_xor);
+        // then lane (sample, i) writes checks (r, i).  The per-check L-term XOR over the staged
+        // bytes cost ~450 VALU per P61 sample at any p.
         const int P = a.P, L = LT > 0 ? LT : a.L;
+        const int m = a.mX + a.mZ, nsw = (m + 31) / 32;
+        uint32_t* __restrict__ syn = reinterpret_cast<uint32_t*>(mc_smem + (size_t)kMcWaves * S * 2 * npad) +
+                                     (size_t)wv * S * nsw;
+        for (int t = lane; t < ns * nsw; t += 64) syn[t] = 0u;
+        wave_sync();
+        const int ng = npad / 4;  // 4-byte words per staged row
+        for (int t = lane; t < ns * 2 * ng; t += 64) {
+            const int sI = qdiv(t, a.magicG2), k = t - sI * 2 * ng;  // word k of [x row | z row]
+            uint32_t word = reinterpret_cast<const uint32_t*>(stage + (size_t)sI * 2 * npad)[k];
+            if (word == 0u) continue;
+            const bool zs = k >= ng;
+            const int R = zs ? a.K : a.J;
+            const int* E = zs ? a.EZ : a.EX;
+            const int c0 = zs ? a.mX : 0;
+            uint32_t* sw = syn + (size_t)sI * nsw;
+            while (word) {
+                const int bt = __builtin_ctz(word) >> 3;
+                word &= ~(0xFFu << (8 * bt));
+                const int v = 4 * (zs ? k - ng : k) + bt;  // qubit (< n: the padding bytes are zero)
+                const int l = v / P, j = v - l * P;
+                for (int r = 0; r < R; ++r) {
+                    const int d = j - E[r * L + l];
+                    const int c = c0 + r * P + (d < 0 ? d + P : d);  // check (r, (j - E) mod P) holds the qubit
+                    atomicXor(&sw[c >> 5], 1u << (c & 31));
+                }
+            }
+        }
+        wave_sync();
         for (int t = lane; t < ns * P; t += 64) {
             const int sI = qdiv(t, a.magicP), i = t - sI * P;
             const long long b = b0 + sI;
-            const uint8_t* ex = stage + (size_t)sI * 2 * npad;
+            const uint32_t* sw = syn + (size_t)sI * nsw;
             for (int r = 0; r < a.J + a.K; ++r) {
                 const bool zs = r >= a.J;
-                const uint8_t* e = zs ? ex + npad : ex;
-                const int* E = zs ? a.EZ + (r - a.J) * L : a.EX + r * L;
-                uint32_t x = 0;
-                if constexpr (LT > 0) {
-#pragma unroll
-                    for (int l = 0; l < LT; ++l) {
-                        const uint32_t j = (uint32_t)(E[l] + i);
-                        x ^= e[l * P + min(j, j - (uint32_t)P)];  // (E + i) mod P: j - P wraps above j when j < P
-                    }
-                } else {
-                    for (int l = 0; l < L; ++l) {
-                        const uint32_t j = (uint32_t)(E[l] + i);
-                        x ^= e[l * P + min(j, j - (uint32_t)P)];
-                    }
-                }
-                if (zs) a.sZ[b * a.mZ + (r - a.J) * P + i] = (uint8_t)(x & 1u);
-                else a.sX[b * a.mX + r * P + i] = (uint8_t)(x & 1u);
+                const int c = (zs ? a.mX + (r - a.J) * P : r * P) + i;
+                const uint8_t x = (uint8_t)((sw[c >> 5] >> (c & 31)) & 1u);
+                if (zs) a.sZ[b * a.mZ + (r - a.J) * P + i] = x;
+                else a.sX[b * a.mX + r * P + i] = x;
             }
         }
     }
@@ -473,13 +493,14 @@ int launch_mc_errors_syndrome(int src, const McArgsHost& h, hipStream_t st)
     }
     const int npad = 8 * a.nb;
     a.S = (a.chkVar == nullptr && c.P > 0 && c.P < 64) ? 64 / c.P : 1;
-    if ((size_t)a.S * 2 * npad > 4096) a.S = 1;
+    if ((size_t)a.S * (2 * npad + 4 * ((c.mX + c.mZ + 31) / 32)) > 4096) a.S = 1;
     auto magic = [](long long d) { return d > 1 ? (uint32_t)(((1ull << 32) + (uint64_t)d - 1) / (uint64_t)d) : 0u; };
-    a.magicW = magic(h.W); a.magicG = magic(npad / 4); a.magicN = magic(npad); a.magicM = magic(c.mX + c.mZ);
+    a.magicW = magic(h.W); a.magicG = magic(npad / 4); a.magicG2 = magic(npad / 2); a.magicN = magic(npad);
+    a.magicM = magic(c.mX + c.mZ);
     a.magicP = magic(c.P); a.magicB = magic(2 * a.nb);
     if ((long long)a.S * std::max<long long>({(long long)h.W, npad, (long long)c.mX + c.mZ}) >= 65536)
         return fail(QEC_ERR_UNSUPPORTED, "mc front end: code too long");
-    const size_t smem = (size_t)kMcWaves * a.S * 2 * npad;
+    const size_t smem = (size_t)kMcWaves * a.S * (2 * npad + 4 * ((c.mX + c.mZ + 31) / 32));  // error rows + syndrome bits
     if (smem > 64 * 1024) return fail(QEC_ERR_UNSUPPORTED, "mc front end: code too long for the LDS stage");
     const long long per_block = (long long)kMcWaves * a.S;
     const dim3 grid((unsigned)((h.B + per_block - 1) / per_block)), block(64 * kMcWaves);

@@ -14,6 +14,7 @@ common() {
   if [ ! -f $obj ] || [ $src -nt $obj ]; then $HIPCC $BASE "$@" -c $src -o $obj; fi
 }
 common qec_ldpc_amd/csrc/code_model.cpp -x c++ &
+common qec_ldpc_amd/csrc/cpu_engine.cpp -x c++ &
 common qec_ldpc_amd/csrc/montecarlo.hip &
 common qec_ldpc_amd/csrc/capi.cpp -x hip &
 common qec_ldpc_amd/csrc/bp_sparse.hip &
@@ -26,7 +27,9 @@ build() {
   $HIPCC $BASE -DQEC_KBENCH_MINIMAL "$@" -c qec_ldpc_amd/csrc/bp_decode.hip -o $out/bp_decode.o
   $HIPCC $BASE -DQEC_KBENCH_MINIMAL -mllvm -amdgpu-sched-strategy=iterative-minreg "$@" \
       -c qec_ldpc_amd/csrc/bp_decode_p61.hip -o $out/bp_decode_p61.o
-  $HIPCC --offload-arch=gfx950 -shared -fPIC -o $out/libqecldpc.so $out/bp_decode.o $out/bp_decode_p61.o $COMMON/*.o
+  $HIPCC $BASE -DQEC_KBENCH_MINIMAL "$@" -c qec_ldpc_amd/csrc/bp_decode_phase.hip -o $out/bp_decode_phase.o
+  $HIPCC --offload-arch=gfx950 -shared -fPIC -o $out/libqecldpc.so $out/bp_decode.o $out/bp_decode_p61.o \
+      $out/bp_decode_phase.o $COMMON/*.o
   echo "built $name"
 }
 pids=()

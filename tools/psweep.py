@@ -49,6 +49,8 @@ def main():
     ap.add_argument("--batch", type=int, default=65536)
     ap.add_argument("--seed", type=lambda v: int(v, 0), default=0x51EC0DE)
     ap.add_argument("--out", default=None, help="write the per-p lines to this JSON file (rank 0)")
+    ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
+                    help="decoder option (qec_decoder_set_option), e.g. schedule=0")
     args = ap.parse_args()
 
     import torch
@@ -67,6 +69,9 @@ def main():
     dev = torch.device("cuda", local)
     code = q.Quantum_LDPC_Code.createFromFile(code_path(args.code))
     dec = q.DecoderGPU(code, local)
+    for kv in args.opt:
+        k, v = kv.split("=")
+        dec.set_option(k, int(v))
     lo, hi = shard_range(args.total, rank, world)
     dec.monte_carlo(args.seed, lo, min(hi - lo, 4096), args.ps[0], args.iters, args.stop, args.batch)  # warm-up
     lines = []

@@ -65,6 +65,15 @@ namespace qec {
 #ifndef QEC_GUARD_MIN
 #define QEC_GUARD_MIN 1
 #endif
+//   QEC_GUARD_ZERO   1: the division guard only excludes numerators in (0, 2^-98) when p' <= 1/2
+//                    (zero_ok); 0: the general guard (numerators and denominators)
+#ifndef QEC_GUARD_ZERO
+#define QEC_GUARD_ZERO 1
+#endif
+//   QEC_GUARD_GLOBAL 1: one bound per soft var pass (short_domain) selects a guard-free pass
+#ifndef QEC_GUARD_GLOBAL
+#define QEC_GUARD_GLOBAL 0
+#endif
 //   QEC_ZEROSKIP     a column whose every numerator is +0 (and denominator > 0) on every live
 //                    lane gets q = +0 without dividing (IEEE: +0 / d = +0 for d > 0)
 #ifndef QEC_ZEROSKIP
@@ -105,26 +114,23 @@ namespace qec {
 #ifndef QEC_LONG_PRIO
 #define QEC_LONG_PRIO 0
 #endif
-//   QEC_ROW_HARD     a soft sector's check pass takes the XOR form row by row: row r of the
-//                    var pass's outputs is tested for hardness on its own (one ballot per output
-//                    into a per-row SGPR mask instead of one OR into a lane register), and a row
-//                    whose every message is +0 or 1.0 is updated by check_pass_hard's rule.
-//                    Bit-identical but slower (P61 0.819 / 0.750 ms for modes 1 / 2 vs 0.706 ms:
-//                    profiles/r01/session7/cmp_s7e_*.txt, cmp_s7f_*.txt): rows rarely harden
-//                    before their whole sector does.  Off.
-#ifndef QEC_ROW_HARD
-#define QEC_ROW_HARD 0
-#endif
+//   (a row-by-row XOR form for rows that harden before their sector, QEC_ROW_HARD, was measured
+//    slower in round 1 -- rows rarely harden before their whole sector does -- and removed)
 //   QEC_SYN_ROWBARRIER  the syndrome test of the syndrome stop rule rotates one row at a time
 #ifndef QEC_SYN_ROWBARRIER
 #define QEC_SYN_ROWBARRIER 1
+#endif
+//   QEC_COL_GROUP    columns per division guard in soft var passes (var_pass); 0: per variant
+#ifndef QEC_COL_GROUP
+#define QEC_COL_GROUP 0
 #endif
 #define QEC_PICK(macro, dflt) ((macro) >= 0 ? (macro) != 0 : (dflt))
 
 // Per-variant tuning: minimum waves per SIMD for the register allocator, and the options above.
 template <int MINW_, bool RELABEL_, bool ZEROSKIP_, bool FASTDIV_, bool SATURATE_ = false, bool SPLIT_ = false,
-          bool MASKSEL_ = false, int PIPE_ = 0, int WPB_ = 4, int SYNW_ = 0>
+          bool MASKSEL_ = false, int PIPE_ = 0, int WPB_ = 4, int SYNW_ = 0, int CG_ = 1>
 struct Tune {
+    static constexpr int kColGroup = QEC_COL_GROUP > 0 ? QEC_COL_GROUP : CG_;  // columns per division guard
     static constexpr int kMinWaves = MINW_;
     static constexpr int kMinWavesSyn = SYNW_ > 0 ? SYNW_ : MINW_;  // the syndrome-stop kernels
     static constexpr int kWavesPerBlock = WPB_;  // waves per workgroup (QEC_WAVES_PER_BLOCK overrides)
@@ -137,9 +143,31 @@ struct Tune {
     static constexpr bool kSaturate = QEC_PICK(QEC_SATURATE, SATURATE_);
 };
 
+// the largest divisor of L not above the variant's column-group size
+template <class TU, int L>
+constexpr int col_group()
+{
+    int g = TU::kColGroup < 1 ? 1 : (TU::kColGroup > L ? L : TU::kColGroup);
+    while (L % g != 0) --g;
+    return g;
+}
+
 // true iff pred holds on every live lane of the wave (lanes outside the batch, or masked off
 // by a finished group, do not vote)
 __device__ __forceinline__ bool all_live(bool pred, bool live) { return __ballot(live && !pred) == 0ull; }
+// The same for a shift provider: with compile-time P > 32 a wave holds one syndrome group whose
+// lanes [0, P) are all live once the wave runs (a wave with no syndrome of the batch returns
+// at entry), so liveness is a constant lane mask instead of a per-lane predicate.
+template <class SH>
+__device__ __forceinline__ bool all_live_sh(bool pred, bool live)
+{
+    if constexpr (SH::kStatic && 2 * SH::kP > 64) {
+        constexpr unsigned long long gm = SH::kP >= 64 ? ~0ull : ((1ull << SH::kP) - 1ull);
+        return (__ballot(!pred) & gm) == 0ull;
+    } else {
+        return all_live(pred, live);
+    }
+}
 
 // The hard-message paths need 0 < p' < 1: then every message lies in [0, 1], zeros are +0,
 // and q - q*q == 0 exactly iff q is +0 or 1 (NaN fails the test).
@@ -406,21 +434,38 @@ __device__ __forceinline__ bool div_short_ok(float n, float d)
     return (d >= 0x1p-98f) & ((__float_as_uint(n) - 1u) >= (__float_as_uint(0x1p-98f) - 1u));
 }
 
+//   QEC_PATH_STATS   experiment builds only: count, per sector, the var-pass columns taking each
+//                    path (same / zero / short division / full division; soft or hard inputs)
+#ifndef QEC_PATH_STATS
+#define QEC_PATH_STATS 0
+#endif
+#ifndef QEC_EXP_SHORTALL
+#define QEC_EXP_SHORTALL 0
+#endif
+#if QEC_PATH_STATS
+static __device__ unsigned long long g_path_stats[24];
+#if defined(QEC_P61_MINREG_TU)
+}  // namespace qec
+extern "C" int qec_debug_path_stats(unsigned long long* out, int reset)
+{
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(qec::g_path_stats), sizeof(qec::g_path_stats)) != hipSuccess) return -1;
+    if (reset) {
+        static const unsigned long long z[24] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(qec::g_path_stats), z, sizeof z) != hipSuccess) return -1;
+    }
+    return 0;
+}
+namespace qec {
+#endif
+#endif
+
 // ---- one sector (X: R = J, Z: R = K) ------------------------------------
 // EqNodeUpdate (DecoderCPU.h:150-186) for checks (r, i), r = 0..R-1: lane-local.
 template <int R, int L>
-__device__ __forceinline__ void check_pass(float (&msg)[R][L], uint32_t sbits, uint32_t hrows = 0)
+__device__ __forceinline__ void check_pass(float (&msg)[R][L], uint32_t sbits)
 {
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-        if (QEC_ROW_HARD && ((hrows >> r) & 1u)) {  // every message of row r is +0 or 1.0: see check_pass_hard
-            uint32_t x = ((sbits >> r) & 1u) ? 0x3F800000u : 0u;
-#pragma unroll
-            for (int l = 0; l < L; ++l) x ^= __float_as_uint(msg[r][l]);
-#pragma unroll
-            for (int l = 0; l < L; ++l) msg[r][l] = __uint_as_float(x ^ __float_as_uint(msg[r][l]));
-            continue;
-        }
         const float h = ((sbits >> r) & 1u) ? 0.5f : -0.5f;
         float av[L];
 #pragma unroll
@@ -469,6 +514,40 @@ __device__ __forceinline__ void check_pass_hard(float (&msg)[R][L], uint32_t sbi
     }
 }
 
+// Zero numerators.  A numerator n = +0 is harmless: then d = P0 = (1 - p') prod (1 - g_k) over F
+// factors, where every 1 - g_k is exact and either 0 or >= 2^-24 (g <= 1 - 2^-24 when g < 1), so
+// d is either 0 (0 / 0: NaN from both sequences) or >= (1 - p') 2^(-24 F), which for p' <= 1/2 and
+// F <= 5 is >= 2^-121: rcp(d) is finite and the short form returns +0, as +0 / d does.  So with
+// zero_ok the guard only has to exclude numerators in (0, 2^-98) (d >= n covers the rest).
+template <int R, bool LAST>
+__device__ __forceinline__ bool zero_ok(float pp)
+{
+    constexpr int F = LAST ? R : R - 1;  // factors in a numerator
+    return F <= 5 && pp >= 0.0f && pp <= 0.5f;
+}
+
+// true iff every division of the coming var pass lies in the short form's domain, on every live
+// lane (zero_ok required): each numerator is a left fold p' * g_a * g_b * ... over F incoming
+// check messages g in [0, 1] (or NaN); if one of them is 0 so is the numerator, and otherwise, as
+// rounding is monotone, the numerator is at least the same fold with every factor replaced by the
+// smallest nonzero incoming message m; when that bound is >= 2^-98 so is every nonzero numerator.
+// A NaN message never lowers m and yields NaN through the short form, as through the IEEE
+// division.  The wave-wide test does not depend on the lane layout, so it runs on the check view.
+template <int R, int L, bool LAST, class SH>
+__device__ __forceinline__ bool short_domain(const float (&msg)[R][L], float pp, bool live)
+{
+    uint32_t m = 0xFFFFFFFFu;  // smallest nonzero message bits, minus one (+0 wraps to the top)
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int l = 0; l < L; ++l) m = min(m, __float_as_uint(msg[r][l]) - 1u);
+    const float mf = m == 0xFFFFFFFFu ? 1.0f : __uint_as_float(m + 1u);
+    float b = pp;
+#pragma unroll
+    for (int k = 0; k < (LAST ? R : R - 1); ++k) b = b * mf;
+    return all_live_sh<SH>((int)(__float_as_uint(b) >= __float_as_uint(0x1p-98f)) & (int)zero_ok<R, LAST>(pp), live);
+}
+
 // VarNodeUpdate (DecoderCPU.h:188-229) for variables (l, i): gather the R incoming
 // check messages by forward rotation, update, scatter back by the inverse rotation.
 // LAST: the final iteration includes the self message (DecoderCPU.h:216).
@@ -477,20 +556,21 @@ __device__ __forceinline__ void check_pass_hard(float (&msg)[R][L], uint32_t sbi
 // outgoing one (only tracked when the hard-message paths are enabled for this launch).
 // vagree (out, meaningful when hard comes out set): every variable's R outgoing messages are
 // equal (on every live lane), i.e. the new state passes var_pass_agree's test as it stands.
-template <int R, int L, int SEC, bool LAST, bool HD, class SH, class TU>
+// CG: columns per division guard.  The guard chooses, wave-uniformly, between the short and the
+// IEEE division sequence, and each such branch ends a basic block; with CG columns per guard the
+// compiler schedules CG columns' products, divisions and rotations as one straight-line block.
+// CG > 1 requires soft inputs (hard == false on entry): the hard-input agreement shortcut below
+// works column by column.
+// ALLFAST: the caller proved every division of this pass inside the short form's domain
+// (short_domain below), so no column evaluates the guard: the pass is straight-line code.
+template <int R, int L, int SEC, bool LAST, bool HD, class SH, class TU, int CG = 1, bool ALLFAST = false>
 __device__ __forceinline__ uint32_t var_pass(const BpArgs& a, float (&msg)[R][L], const Lane& ln, float pp,
-                                             float one_minus_pp, bool& hard, bool& vagree, uint32_t& hrows,
-                                             bool track = true)
+                                             float one_minus_pp, bool& hard, bool& vagree, bool track = true)
 {
-    const bool hard_in = hard;
+    static_assert(L % CG == 0, "column groups must tile the L columns");
+    const bool hard_in = CG == 1 && hard;
     bool vsame = true;  // this lane's variables: all R outputs equal (float compare: NaN is unequal)
-    uint32_t soft_bits = 0;  // OR of bits(q - q*q) over outputs not known to be hard: 0 iff all are 0 or 1
-    // QEC_ROW_HARD 1: live lanes with a soft output in row r (wave masks, a ballot per output);
-    //              2: OR of bits(q - q*q) over row r's outputs (a lane register per row, R ballots)
-    unsigned long long rsoft[R];
-    uint32_t rbits[R];
-#pragma unroll
-    for (int r = 0; r < R; ++r) { rsoft[r] = 0ull; rbits[r] = 0u; }
+    uint32_t soft_bits = 0;  // OR of bits(q - q*q) over the outputs: 0 iff all are 0 or 1
     // the short division's guard assumes every message is a probability in [0, 1], which
     // holds by induction when p' is (DecoderCPU.h:135-229); other p' always take the full path
     const bool pp_ok = pp >= 0.0f && pp <= 1.0f;
@@ -499,8 +579,9 @@ __device__ __forceinline__ uint32_t var_pass(const BpArgs& a, float (&msg)[R][L]
     uint32_t hdmask = 0;
     // QEC_PIPELINE = D: the gathers of columns l + 1 .. l + D are in flight while column l is
     // computed, so their ds_bpermute latency hides behind column l's arithmetic in the same wave
-    // (the per-column uniform branches below end basic blocks, so the compiler cannot do this).
+    // (the per-group uniform branches below end basic blocks, so the compiler cannot do this).
     constexpr int D = TU::kPipeline > 0 ? (TU::kPipeline < L ? TU::kPipeline : L - 1) : 0;
+    constexpr int ND = LAST ? 1 : R;  // distinct outgoing messages per variable (LAST: one, shared)
     float gq[D > 0 ? D : 1][R];  // gq[k]: gathers of column l + 1 + k
     if constexpr (D > 0) {
 #pragma unroll
@@ -509,162 +590,200 @@ __device__ __forceinline__ uint32_t var_pass(const BpArgs& a, float (&msg)[R][L]
             for (int r = 0; r < R; ++r) gq[k][r] = rot<SH>(msg[r][k], ln, SH::template shift<SEC, L>(et, r, k));
     }
 #pragma unroll
-    for (int l = 0; l < L; ++l) {
-        float gv[R], bv[R], qv[R];
-        if constexpr (D > 0) {
+    for (int l0 = 0; l0 < L; l0 += CG) {
+        float gv[CG][R], qv[CG][R];
 #pragma unroll
-            for (int r = 0; r < R; ++r) gv[r] = gq[0][r];
+        for (int c = 0; c < CG; ++c) {
+            const int l = l0 + c;
+            if constexpr (D > 0) {
 #pragma unroll
-            for (int k = 0; k + 1 < D; ++k)
+                for (int r = 0; r < R; ++r) gv[c][r] = gq[0][r];
 #pragma unroll
-                for (int r = 0; r < R; ++r) gq[k][r] = gq[k + 1][r];
-            if (l + D < L) {
+                for (int k = 0; k + 1 < D; ++k)
 #pragma unroll
-                for (int r = 0; r < R; ++r)
-                    gq[D - 1][r] = rot<SH>(msg[r][l + D], ln, SH::template shift<SEC, L>(et, r, l + D));
+                    for (int r = 0; r < R; ++r) gq[k][r] = gq[k + 1][r];
+                if (l + D < L) {
+#pragma unroll
+                    for (int r = 0; r < R; ++r)
+                        gq[D - 1][r] = rot<SH>(msg[r][l + D], ln, SH::template shift<SEC, L>(et, r, l + D));
+                }
+            } else {
+#pragma unroll
+                for (int r = 0; r < R; ++r) gv[c][r] = rot<SH>(msg[r][l], ln, SH::template shift<SEC, L>(et, r, l));
             }
-        } else {
-#pragma unroll
-            for (int r = 0; r < R; ++r) gv[r] = rot<SH>(msg[r][l], ln, SH::template shift<SEC, L>(et, r, l));
         }
         // hard inputs: q_j = P1 / (P0 + P1) with every factor 0 or 1 is exactly the common value
         // when all R inputs agree (all 1: p'/p' = 1; all 0: +0/(1-p') = +0); columns where some
         // variable's inputs disagree (0/0 = NaN) take the arithmetic path below
         bool done = false;
-        if constexpr (TU::kSaturate) {
+        if constexpr (TU::kSaturate && CG == 1) {
             if (hard_in && (LAST || R >= 2)) {
-                const uint32_t x0 = __float_as_uint(gv[0]);
+                const uint32_t x0 = __float_as_uint(gv[0][0]);
                 bool same = true;
 #pragma unroll
-                for (int r = 1; r < R; ++r) same &= __float_as_uint(gv[r]) == x0;
-                if (all_live(same, ln.live)) {
+                for (int r = 1; r < R; ++r) same &= __float_as_uint(gv[0][r]) == x0;
+                if (all_live_sh<SH>(same, ln.live)) {
 #pragma unroll
-                    for (int r = 0; r < R; ++r) qv[r] = gv[0];
+                    for (int r = 0; r < R; ++r) qv[0][r] = gv[0][0];
                     done = true;
+#if QEC_PATH_STATS
+                    if (__lane_id() == 0) atomicAdd(&g_path_stats[SEC * 8 + 4], 1ull);
+#endif
                 }
             }
         }
         if (!done) {
+            // numerators / denominators of the outgoing messages, left folds in ascending k
+            float num[CG][ND], den[CG][ND];
 #pragma unroll
-        for (int r = 0; r < R; ++r) bv[r] = 1.0f - gv[r];
-        // numerators / denominators of the R outgoing messages (LAST: one, shared)
-        constexpr int ND = LAST ? 1 : R;
-        float num[ND], den[ND];
-        if constexpr (LAST) {
-            float P0 = one_minus_pp, P1 = pp;
+            for (int c = 0; c < CG; ++c) {
+                float bv[R];
 #pragma unroll
-            for (int k = 0; k < R; ++k) { P0 = P0 * bv[k]; P1 = P1 * gv[k]; }
-            num[0] = P1;
-            den[0] = P0 + P1;
-        } else {
-            float pre0 = one_minus_pp, pre1 = pp;
+                for (int r = 0; r < R; ++r) bv[r] = 1.0f - gv[c][r];
+                if constexpr (LAST) {
+                    float P0 = one_minus_pp, P1 = pp;
 #pragma unroll
-            for (int j = 0; j < R; ++j) {
-                float t0 = pre0, t1 = pre1;
+                    for (int k = 0; k < R; ++k) { P0 = P0 * bv[k]; P1 = P1 * gv[c][k]; }
+                    num[c][0] = P1;
+                    den[c][0] = P0 + P1;
+                } else {
+                    float pre0 = one_minus_pp, pre1 = pp;
 #pragma unroll
-                for (int k = j + 1; k < R; ++k) { t0 = t0 * bv[k]; t1 = t1 * gv[k]; }
-                num[j] = t1;
-                den[j] = t0 + t1;
-                if (j + 1 < R) { pre0 = pre0 * bv[j]; pre1 = pre1 * gv[j]; }
-            }
-        }
-        float qd[ND];
-        bool zero = false, fast = false;
-        if constexpr (TU::kZeroSkip) {
-            uint32_t nb = 0;
-            bool dpos = true;
+                    for (int j = 0; j < R; ++j) {
+                        float t0 = pre0, t1 = pre1;
 #pragma unroll
-            for (int j = 0; j < ND; ++j) {
-                nb |= __float_as_uint(num[j]);
-                dpos &= den[j] > 0.0f;
-            }
-            zero = all_live(nb == 0u && dpos, ln.live);
-        }
-        if constexpr (TU::kFastDiv) {
-            if (!zero) {
-#if QEC_GUARD_MIN
-                // the guard of every division of the column at once, as unsigned minima of bit
-                // patterns (non-negative floats order like their bits): numerators minus 1 (+0
-                // wraps to the top), denominators as they are.  A NaN sorts above every number, so
-                // it never fails the guard; the short form then returns NaN, as the IEEE division
-                // does.
-                uint32_t nm = 0xFFFFFFFFu, dm = 0xFFFFFFFFu;
-#pragma unroll
-                for (int j = 0; j < ND; ++j) {
-                    nm = min(nm, __float_as_uint(num[j]) - 1u);
-                    dm = min(dm, __float_as_uint(den[j]));
+                        for (int k = j + 1; k < R; ++k) { t0 = t0 * bv[k]; t1 = t1 * gv[c][k]; }
+                        num[c][j] = t1;
+                        den[c][j] = t0 + t1;
+                        if (j + 1 < R) { pre0 = pre0 * bv[j]; pre1 = pre1 * gv[c][j]; }
+                    }
                 }
-                const bool ok = (int)(dm >= __float_as_uint(0x1p-98f)) & (int)(nm >= __float_as_uint(0x1p-98f) - 1u);
-#else
-                bool ok = true;
+            }
+            float qd[CG][ND];
+            bool zero = false, fast = false;
+            if constexpr (TU::kZeroSkip && !ALLFAST) {
+                uint32_t nb = 0;
+                bool dpos = true;
 #pragma unroll
-                for (int j = 0; j < ND; ++j) ok &= div_short_ok(num[j], den[j]);
+                for (int c = 0; c < CG; ++c)
+#pragma unroll
+                    for (int j = 0; j < ND; ++j) {
+                        nb |= __float_as_uint(num[c][j]);
+                        dpos &= den[c][j] > 0.0f;
+                    }
+                zero = all_live(nb == 0u && dpos, ln.live);
+            }
+            if constexpr (ALLFAST) {
+                fast = true;
+            } else if constexpr (TU::kFastDiv) {
+                if constexpr (QEC_GUARD_ZERO != 0) {
+                    // numerators outside (0, 2^-98): minima of their bit patterns minus one, +0
+                    // wrapping to the top.  Needs zero_ok (p' <= 1/2, a wave-uniform AND, no
+                    // branch); other p' (p > 3/4, never a decoding regime) always take the IEEE
+                    // division.
+                    uint32_t nm = 0xFFFFFFFFu;
+#pragma unroll
+                    for (int c = 0; c < CG; ++c)
+#pragma unroll
+                        for (int j = 0; j < ND; ++j) nm = min(nm, __float_as_uint(num[c][j]) - 1u);
+                    fast = all_live_sh<SH>((int)(nm >= __float_as_uint(0x1p-98f) - 1u) & (int)zero_ok<R, LAST>(pp), ln.live);
+                } else if (!zero) {
+                    // the guard of every division of the group at once, as unsigned minima of bit
+                    // patterns (non-negative floats order like their bits): numerators minus 1 (+0
+                    // wraps to the top), denominators as they are.  A NaN sorts above every
+                    // number, so it never fails the guard; the short form then returns NaN, as the
+                    // IEEE division does.
+                    uint32_t nm = 0xFFFFFFFFu, dm = 0xFFFFFFFFu;
+#pragma unroll
+                    for (int c = 0; c < CG; ++c)
+#pragma unroll
+                        for (int j = 0; j < ND; ++j) {
+                            nm = min(nm, __float_as_uint(num[c][j]) - 1u);
+                            dm = min(dm, __float_as_uint(den[c][j]));
+                        }
+                    const bool ok = (int)(dm >= __float_as_uint(0x1p-98f)) & (int)(nm >= __float_as_uint(0x1p-98f) - 1u);
+                    fast = pp_ok && all_live_sh<SH>(ok, ln.live);
+                }
+            }
+#if QEC_EXP_SHORTALL
+            fast = pp_ok && !zero;  // timing experiment only: the guard ignored (outputs may differ)
 #endif
-                fast = pp_ok && all_live(ok, ln.live);
+#if QEC_PATH_STATS
+            if (__lane_id() == 0)
+                atomicAdd(&g_path_stats[SEC * 8 + (hard_in ? 4 : 0) + (zero ? 1 : fast ? 2 : 3)], (unsigned long long)CG);
+            {
+                // guard anatomy of the group: every n >= 2^-98 / zeros but no tiny nonzero n and every
+                // d >= 2^-98 / a tiny nonzero n / some d < 2^-98
+                bool anyz = false, tiny = false, dsmall = false, allbig = true;
+#pragma unroll
+                for (int c = 0; c < CG; ++c)
+#pragma unroll
+                    for (int j = 0; j < ND; ++j) {
+                        const uint32_t nb = __float_as_uint(num[c][j]);
+                        anyz |= nb == 0u;
+                        tiny |= nb != 0u && nb < __float_as_uint(0x1p-98f);
+                        dsmall |= __float_as_uint(den[c][j]) < __float_as_uint(0x1p-98f);
+                        allbig &= nb >= __float_as_uint(0x1p-98f);
+                    }
+                const bool wz = __ballot(anyz && ln.live) != 0ull, wt = __ballot(tiny && ln.live) != 0ull;
+                const bool wd = __ballot(dsmall && ln.live) != 0ull, wb = __ballot(!allbig && ln.live) == 0ull;
+                const int k = wb ? 0 : wt ? 2 : wd ? 3 : wz ? 1 : 3;
+                if (__lane_id() == 0 && !hard_in) atomicAdd(&g_path_stats[16 + SEC * 4 + k], (unsigned long long)CG);
             }
-        }
-        if (zero) {
+#endif
+            if (zero) {
 #pragma unroll
-            for (int j = 0; j < ND; ++j) qd[j] = 0.0f;
-        } else if (fast) {
+                for (int c = 0; c < CG; ++c)
 #pragma unroll
-            for (int j = 0; j < ND; ++j) qd[j] = div_short(num[j], den[j]);
-        } else {
+                    for (int j = 0; j < ND; ++j) qd[c][j] = 0.0f;
+            } else if (fast) {
 #pragma unroll
-            for (int j = 0; j < ND; ++j) qd[j] = num[j] / den[j];
-        }
-        if constexpr (TU::kSaturate) {
-            if (!zero && track) {
+                for (int c = 0; c < CG; ++c)
 #pragma unroll
-                for (int j = 0; j < ND; ++j) {
-                    const uint32_t sb = __float_as_uint(__builtin_fmaf(-qd[j], qd[j], qd[j]));
-                    if constexpr (QEC_ROW_HARD == 1 && !LAST)
-                        rsoft[j] |= __ballot(ln.live && sb != 0u);
-                    else if constexpr (QEC_ROW_HARD == 2 && !LAST)
-                        rbits[j] |= sb;
-                    else
-                        soft_bits |= sb;
+                    for (int j = 0; j < ND; ++j) qd[c][j] = div_short(num[c][j], den[c][j]);
+            } else {
+#pragma unroll
+                for (int c = 0; c < CG; ++c)
+#pragma unroll
+                    for (int j = 0; j < ND; ++j) qd[c][j] = num[c][j] / den[c][j];
+            }
+            if constexpr (TU::kSaturate) {
+                if (!zero && track) {
+#pragma unroll
+                    for (int c = 0; c < CG; ++c) {
+#pragma unroll
+                        for (int j = 0; j < ND; ++j)
+                            soft_bits |= __float_as_uint(__builtin_fmaf(-qd[c][j], qd[c][j], qd[c][j]));
+#pragma unroll
+                        for (int j = 1; j < ND; ++j) vsame &= qd[c][j] == qd[c][0];
+                    }
                 }
-#pragma unroll
-                for (int j = 1; j < ND; ++j) vsame &= qd[j] == qd[0];
             }
-        }
 #pragma unroll
-        for (int r = 0; r < R; ++r) qv[r] = qd[LAST ? 0 : r];
+            for (int c = 0; c < CG; ++c)
+#pragma unroll
+                for (int r = 0; r < R; ++r) qv[c][r] = qd[c][LAST ? 0 : r];
         }  // !done
-        if constexpr (HD) {
-            bool hd = false;
 #pragma unroll
-            for (int r = 0; r < R; ++r) hd |= (qv[r] >= 0.5f);
-            hdmask |= (uint32_t)hd << l;
-        }
+        for (int c = 0; c < CG; ++c) {
+            const int l = l0 + c;
+            if constexpr (HD) {
+                bool hd = false;
 #pragma unroll
-        for (int r = 0; r < R; ++r) {
-            const int sh = SH::template shift<SEC, L>(et, r, l);
-            msg[r][l] = rot<SH>(qv[r], ln, sh == 0 ? 0 : P - sh);
+                for (int r = 0; r < R; ++r) hd |= (qv[c][r] >= 0.5f);
+                hdmask |= (uint32_t)hd << l;
+            }
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const int sh = SH::template shift<SEC, L>(et, r, l);
+                msg[r][l] = rot<SH>(qv[c][r], ln, sh == 0 ? 0 : P - sh);
+            }
         }
     }
     if constexpr (TU::kSaturate) {
         const bool forms = track && (a.hardPaths & QEC_HP_FORMS) && hard_ok(pp);
-        if constexpr (QEC_ROW_HARD == 2 && !LAST) {
-#pragma unroll
-            for (int r = 0; r < R; ++r) rsoft[r] = __ballot(ln.live && rbits[r] != 0u);
-        }
-        if constexpr (QEC_ROW_HARD && !LAST) {
-            unsigned long long any = 0ull;
-            uint32_t hr = 0;
-#pragma unroll
-            for (int r = 0; r < R; ++r) {
-                any |= rsoft[r];
-                hr |= (uint32_t)(rsoft[r] == 0ull) << r;
-            }
-            hard = forms && any == 0ull;
-            hrows = forms ? hr : 0u;
-        } else {
-            hard = forms && all_live(soft_bits == 0u, ln.live);
-            hrows = 0u;
-        }
-        vagree = hard && all_live(vsame, ln.live);
+        hard = forms && all_live_sh<SH>(soft_bits == 0u, ln.live);
+        vagree = hard && all_live_sh<SH>(vsame, ln.live);
     }
     return hdmask;
 }
@@ -691,7 +810,7 @@ __device__ __forceinline__ bool var_pass_agree(const BpArgs& a, const float (&ms
         if constexpr (HD) hd |= (uint32_t)(x0 == 0x3F800000u) << l;  // q >= 0.5f <=> q == 1.0f here
     }
     hdmask = hd;
-    return all_live(same, ln.live);
+    return all_live_sh<SH>(same, ln.live);
 }
 
 // CheckConvergence (DecoderCPU.h:231-246) on this lane's edges.
@@ -741,7 +860,7 @@ __device__ __forceinline__ bool lane_syndrome_ok(const BpArgs& a, uint32_t hdmas
 template <int R, int L, int SEC, int STOP, bool LAST, class SH, class TU>
 __device__ __forceinline__ bool iteration(const BpArgs& a, float (&msg)[R][L], uint32_t sbits, int n, Lane& ln,
                                           float pp, float one_minus_pp, bool& hard, bool& agreed, bool& vagree,
-                                          uint32_t& hrows, uint32_t& hd_out)
+                                          uint32_t& hd_out)
 {
     const int P = SH::P(a);
     // launder the permute bases so their per-rotation selects are recomputed inside the
@@ -757,13 +876,18 @@ __device__ __forceinline__ bool iteration(const BpArgs& a, float (&msg)[R][L], u
         if (agreed)
             vagree = true;
         else
-            hdmask = var_pass<R, L, SEC, LAST, HD, SH, TU>(a, msg, ln, pp, one_minus_pp, hard, vagree, hrows);
+            hdmask = var_pass<R, L, SEC, LAST, HD, SH, TU>(a, msg, ln, pp, one_minus_pp, hard, vagree);
     } else {
-        check_pass<R, L>(msg, sbits, hrows);
+        check_pass<R, L>(msg, sbits);
         // the hard-state test is skipped in the first QEC_TRACK_FROM iterations (they essentially
         // never end hard; skipping only delays the exact hard forms, never changes a bit)
-        hdmask = var_pass<R, L, SEC, LAST, HD, SH, TU>(a, msg, ln, pp, one_minus_pp, hard, vagree, hrows,
-                                                       LAST || n >= QEC_TRACK_FROM);
+        // hard == false here, so the soft inputs allow column groups (var_pass)
+        constexpr int CG = col_group<TU, L>();
+        const bool track = LAST || n >= QEC_TRACK_FROM;
+        if (QEC_GUARD_GLOBAL && TU::kFastDiv && zero_ok<R, LAST>(pp) && short_domain<R, L, LAST, SH>(msg, pp, ln.live))
+            hdmask = var_pass<R, L, SEC, LAST, HD, SH, TU, CG, true>(a, msg, ln, pp, one_minus_pp, hard, vagree, track);
+        else
+            hdmask = var_pass<R, L, SEC, LAST, HD, SH, TU, CG>(a, msg, ln, pp, one_minus_pp, hard, vagree, track);
     }
     if constexpr (STOP == QEC_STOP_REF) {
         if (n % 10 == 0) return group_all_sh<SH>(lane_converged<R, L>(msg), ln, P);  // DecoderCPU.h:287-290
@@ -962,7 +1086,6 @@ __device__ __forceinline__ void decode_sector(const BpArgs& a, Lane& ln, uint32_
     // can read it lane-locally
     bool in_agree = false, st_agreed = false;
     bool agreed = false, vagree = false;
-    uint32_t hrows = 0;  // QEC_ROW_HARD: rows of the current state whose every message is +0 or 1.0
     int ph_soft = 0, ph_hard = 0, ph_agree = 0, ph_jump = 0;  // QEC_PHASE_STATS
     // syndrome stop rule: the hard decision of the last executed iteration and its syndrome test
     // (hd_valid: the current state is that iteration's output, i.e. not reached by a cycle jump).
@@ -988,7 +1111,7 @@ __device__ __forceinline__ void decode_sector(const BpArgs& a, Lane& ln, uint32_
             ++it;
             const bool was_hard = hard;
             syn_last = iteration<R, L, SEC, STOP, false, SH, TU>(a, msg, sbits, n, ln, pp, one_minus_pp, hard, agreed,
-                                                                 vagree, hrows, hd_last);
+                                                                 vagree, hd_last);
             hd_valid = true;
             if (syn_last) active = false;
             if constexpr (QEC_PHASE_STATS) { ph_soft += !was_hard; ph_hard += was_hard && !agreed; ph_agree += agreed; }
@@ -1013,7 +1136,7 @@ __device__ __forceinline__ void decode_sector(const BpArgs& a, Lane& ln, uint32_
         ++it;
         const bool was_hard = hard;
         syn_last = iteration<R, L, SEC, STOP, true, SH, TU>(a, msg, sbits, n, ln, pp, one_minus_pp, hard, agreed, vagree,
-                                                            hrows, hd_last);
+                                                            hd_last);
         hd_valid = true;
         if constexpr (QEC_PHASE_STATS) { ph_soft += !was_hard; ph_hard += was_hard && !agreed; ph_agree += agreed; }
         st_agreed = vagree;

@@ -101,6 +101,11 @@ namespace qec {
 #ifndef QEC_TABLE0
 #define QEC_TABLE0 1
 #endif
+//   QEC_ZERO_SYNDROME  syndrome stop: a sector whose syndrome is zero on every live lane of the wave
+//                      skips to its known outputs (decode_sector)
+#ifndef QEC_ZERO_SYNDROME
+#define QEC_ZERO_SYNDROME 1
+#endif
 //   QEC_TRACK_FROM   first iteration whose var pass tests whether the sector became hard
 #ifndef QEC_TRACK_FROM
 #define QEC_TRACK_FROM 2
@@ -1066,6 +1071,28 @@ __device__ __forceinline__ void decode_sector(const BpArgs& a, Lane& ln, uint32_
 {
     const int i = ln.i;
     const int P = SH::P(a);
+
+    // Zero syndrome under the syndrome stop rule (most sectors at low p: P61 at p = 0.002, 44 %):
+    // iteration 0 (by table, see iteration0) sends every edge the pattern-0 entry tab0[r], so the
+    // hard decision is 0 when every tab0[r] < 0.5, its syndrome is the input's (0), and the sector
+    // stops after that iteration with e = 0, conv = every tab0[r] outside (0.01, 0.99).  The same
+    // outputs without the iteration's rotations (not when the final messages are requested).
+    if constexpr (STOP == QEC_STOP_SYNDROME && QEC_TABLE0 && QEC_ZERO_SYNDROME) {
+        if (a.maxIter >= 2 && a.q == nullptr && all_live(sbits == 0u, in_range)) {
+            bool low = true, cv = true;
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                low &= tab0[r] < 0.5f;
+                cv &= outside(tab0[r]);
+            }
+            if (low) {  // wave-uniform (tab0 is the workgroup's)
+                emit_decisions<L, SEC, SH>(a, ln, b, in_range, 0u, stage);
+                if (!cv) flags |= SEC ? QEC_CONVERGENCE_FAIL_Z : QEC_CONVERGENCE_FAIL_X;
+                iters_out = 1;
+                return;
+            }
+        }
+    }
 
     // InitVarNodes: every edge starts at p' (DecoderCPU.h:135-148, 265-267)
     float msg[R][L];

@@ -345,6 +345,7 @@ void* sparse_plan_create(const Code& c, int device)
 }
 
 const int32_t* sparse_plan_chkvar(const void* plan) { return static_cast<const SparsePlan*>(plan)->chkVar.data(); }
+const int32_t* sparse_plan_varedge(const void* plan) { return static_cast<const SparsePlan*>(plan)->varEdge.data(); }
 
 int launch_decode_sparse(void* plan, const uint8_t* sX, const uint8_t* sZ, long long B, float errorProbability,
                          int maxIter, int stop, uint8_t* eX, uint8_t* eZ, uint8_t* flags, int32_t* iters, float* q,

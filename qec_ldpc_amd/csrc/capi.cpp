@@ -34,6 +34,7 @@ void* sparse_plan_create(const Code& c, int device);
 void sparse_plan_free(void* plan);
 const char* sparse_plan_name(const void* plan);
 const int32_t* sparse_plan_chkvar(const void* plan);
+const int32_t* sparse_plan_varedge(const void* plan);
 int launch_decode_sparse(void* plan, const uint8_t* sX, const uint8_t* sZ, long long B, float errorProbability,
                          int maxIter, int stop, uint8_t* eX, uint8_t* eZ, uint8_t* flags, int32_t* iters, float* q,
                          hipStream_t stream);
@@ -505,6 +506,11 @@ const int32_t* syndrome_table(const qec_decoder* d)
     return d->engine == QEC_ENGINE_SPARSE ? sparse_plan_chkvar(d->sparse) : nullptr;
 }
 
+const int32_t* variable_table(const qec_decoder* d)
+{
+    return d->engine == QEC_ENGINE_SPARSE ? sparse_plan_varedge(d->sparse) : nullptr;
+}
+
 int check_decode_args(const qec_decoder* d, const void* sX, const void* sZ, size_t B, int stop)
 {
     if (!d) return fail(QEC_ERR_ARG, "decode: null decoder");
@@ -682,6 +688,7 @@ int mc_batch(qec_decoder* d, McArgsHost h, int src, float p, int maxIter, int st
     h.code = d->code.get();
     h.sX = d->msX.data(); h.sZ = d->msZ.data(); h.errp = d->merrp.data();
     h.chkVar = syndrome_table(d);
+    h.varEdge = variable_table(d);
     int rc = launch_mc_errors_syndrome(src, h, st);
     if (rc) return rc;
     if (ev0) QEC_HIP_CHECK(hipEventRecord(ev0, st));
@@ -994,6 +1001,7 @@ int qec_sample_syndrome_dev(qec_decoder* d, uint64_t seed, uint64_t start, size_
     h.seed = seed; h.start = start; h.p = p;
     h.sX = sX; h.sZ = sZ; h.errp = errp;
     h.chkVar = syndrome_table(d);
+    h.varEdge = variable_table(d);
     h.B = (long long)B;
     return launch_mc_errors_syndrome(MC_SRC_PHILOX, h, static_cast<hipStream_t>(stream));
 }

@@ -15,7 +15,9 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdint>
+#include <cstdlib>
 
 #include "qec_device.h"
 #include "qec_internal.h"
@@ -41,71 +43,111 @@ __host__ __device__ inline U4 philox4x32_10(U4 c, uint32_t k0, uint32_t k1)
     return c;
 }
 
-constexpr uint32_t kPhiloxSalt = 0x51EC0DE5u;
 
-// Depolarising sampler.  Qubits 4g .. 4g+3 of sample b share one Philox call: counter
-// (b_lo, b_hi, g, salt), key (seed_lo, seed_hi), output words w0..w3, word j for qubit 4g + j.
-// The qubit is hit iff w < thr = floor(p 2^32) (saturated at 2^32).  Given a hit, w is uniform on
-// [0, thr), and its type is t = floor(w mul / 2^64) with mul = min(floor(3 2^64 / thr), 2^64 - 1),
-// i.e. floor(3 w / thr) up to the rounding of mul: 0 = X, 1 = Y, 2 = Z, each with probability
-// 1/3 to within 1/thr (Y sets both bits).  Four qubits per call: the front end's cost is the
-// Philox rounds.  Restated in numpy by oracle/philox.py.
-struct Depol {
-    uint64_t seed, thr, mul;
+// Depolarising sampler ("gap walk"; restated in numpy by oracle/philox.py).  A qubit is hit with
+// probability thr / 2^32, thr = floor(p 2^32) (saturated at 2^32), independently of the others, so
+// the number of qubits skipped before the next hit is geometric: P(G >= g) = q^g, q = 1 - thr / 2^32.
+// Sample b walks its qubits 0 .. n-1 in order, drawing 32-bit words from Philox calls k = 0, 1, ...
+// (counter (b_lo, b_hi, k, kGapSalt), key (seed_lo, seed_hi), word 4k + j = output word j of call
+// k): u = next word, G = #{g in 1..n : u < T[g]} with the gap table T[g] = floor(q^g 2^32) (q^g by
+// right-to-left binary exponentiation in IEEE double, powsq); skip G qubits; if the walk is still
+// inside the sample, the qubit there is hit, of type t = floor(3 w / 2^32) of the next word w
+// (0 = X, 1 = Y, 2 = Z; Y sets both bits), and the walk goes on from the next qubit.  A sample at
+// p = 0.01 costs ~13 words (four Philox calls) instead of one word per qubit (153 calls for P61).
+constexpr uint32_t kGapSalt = 0x6A9C0DE5u;
+
+__host__ __device__ inline double powsq(double q, int g)
+{
+    double r = 1.0, b = q;
+    for (int e = g; e != 0;) {
+        if (e & 1) r = r * b;
+        e >>= 1;
+        if (e != 0) b = b * b;
+    }
+    return r;
+}
+
+struct GapParams {
+    uint64_t seed;
+    uint64_t thr;     // 0: no qubit is ever hit
+    double q;         // 1 - thr / 2^32 (exact)
+    float inv_l2q;    // 1 / log2(q) (the gap estimate's scale; -0 for q = 0)
 };
 
-__host__ inline Depol make_depol(uint64_t seed, float p)
+__host__ inline GapParams make_gap(uint64_t seed, float p)
 {
     const double pd = p;
-    Depol d{seed, pd <= 0.0 ? 0ull : pd >= 1.0 ? (1ull << 32) : (uint64_t)(pd * 4294967296.0), 0};
-    if (d.thr >= 3) {
-        const unsigned __int128 m = ((unsigned __int128)3 << 64) / d.thr;
-        d.mul = m > ~0ull ? ~0ull : (uint64_t)m;
-    } else if (d.thr > 0) {
-        d.mul = ~0ull;
-    }
-    return d;
+    GapParams g{seed, pd <= 0.0 ? 0ull : pd >= 1.0 ? (1ull << 32) : (uint64_t)(pd * 4294967296.0), 1.0, 0.0f};
+    g.q = (4294967296.0 - (double)g.thr) / 4294967296.0;
+    g.inv_l2q = g.thr == 0 ? 0.0f : (float)(1.0 / std::log2(g.q));
+    return g;
 }
 
-// x4 / z4: the four qubits' bits as bytes (byte j = qubit 4g + j)
-__device__ __forceinline__ void depolarizing4(const Depol& d, uint64_t sb, uint32_t g, uint32_t& x4, uint32_t& z4)
+// The gap before the next hit: #{g in 1..n : u < T[g]} (T non-increasing: q^(g+1) < q^g by far more
+// than the exponentiation's rounding, so this is the largest g with u < T[g], 0 if none).  A float
+// estimate from log2(u / 2^32) / log2(q) lands within a step or two of it; the table walk then
+// makes it exact.  T[1..n] in LDS.
+__device__ __forceinline__ int gap_of(uint32_t u, const uint32_t* __restrict__ T, int n, float inv_l2q)
 {
-    const U4 o = philox4x32_10(U4{(uint32_t)sb, (uint32_t)(sb >> 32), g, kPhiloxSalt}, (uint32_t)d.seed,
-                               (uint32_t)(d.seed >> 32));
-    const uint32_t w[4] = {o.x, o.y, o.z, o.w};
-    x4 = 0;
-    z4 = 0;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        if ((uint64_t)w[j] < d.thr) {
-            // floor(w mul / 2^64) = floor((w mul_hi + floor(w mul_lo / 2^32)) / 2^32), no overflow
-            const uint64_t hi = (uint64_t)w[j] * (d.mul >> 32) + (((uint64_t)w[j] * (uint32_t)d.mul) >> 32);
-            const uint32_t t = (uint32_t)(hi >> 32);
-            x4 |= (uint32_t)(t != 2) << (8 * j);
-            z4 |= (uint32_t)(t != 0) << (8 * j);
+    if (u >= T[1]) return 0;
+    const float x = ((float)u + 0.5f) * 0x1p-32f;
+    const float e = __log2f(x) * inv_l2q;
+    int g = e >= (float)n ? n : e >= 1.0f ? (int)e : 1;
+    while (g < n && u < T[g + 1]) ++g;
+    while (u >= T[g]) --g;  // stops at g = 1 at the latest (u < T[1])
+    return g;
+}
+
+// The walk of one sample (this lane): hit(v, t) for every hit qubit v of type t, in ascending v.
+template <class Hit>
+__device__ __forceinline__ void gap_walk(const GapParams& gp, uint64_t b, int n, const uint32_t* __restrict__ T,
+                                         Hit&& hit)
+{
+    U4 o{0, 0, 0, 0};
+    uint32_t wi = 0, call = 0xFFFFFFFFu;
+    auto next = [&]() -> uint32_t {
+        const uint32_t k = wi >> 2;
+        if (k != call) {
+            o = philox4x32_10(U4{(uint32_t)b, (uint32_t)(b >> 32), k, kGapSalt}, (uint32_t)gp.seed,
+                              (uint32_t)(gp.seed >> 32));
+            call = k;
         }
+        const uint32_t j = wi & 3u;
+        ++wi;
+        return j == 0 ? o.x : j == 1 ? o.y : j == 2 ? o.z : o.w;
+    };
+    int pos = 0;
+    while (true) {
+        pos += gap_of(next(), T, n, gp.inv_l2q);
+        if (pos >= n) break;
+        hit(pos, __umulhi(next(), 3u));
+        if (++pos >= n) break;
     }
 }
 
-// byte form (qec_sample_depolarizing_dev): one thread per four qubits of a sample
-__global__ void sample_depolarizing_kernel(Depol d, uint64_t start, long long B, int n, uint8_t* __restrict__ x,
-                                           uint8_t* __restrict__ z)
+// Build the workgroup's gap table T[1..n] (T[0] unused).
+__device__ __forceinline__ void gap_table(const GapParams& gp, int n, uint32_t* __restrict__ T)
 {
-    const int ng = (n + 3) / 4;
-    const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= B * ng) return;
-    const long long b = t / ng;
-    const int g = (int)(t - b * ng);
-    uint32_t x4, z4;
-    depolarizing4(d, start + (uint64_t)b, (uint32_t)g, x4, z4);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int v = 4 * g + j;
-        if (v < n) {
-            x[b * n + v] = (uint8_t)((x4 >> (8 * j)) & 1u);
-            z[b * n + v] = (uint8_t)((z4 >> (8 * j)) & 1u);
-        }
-    }
+    for (int g = threadIdx.x + 1; g <= n; g += blockDim.x) T[g] = (uint32_t)(powsq(gp.q, g) * 4294967296.0);
+    if (threadIdx.x == 0) T[0] = 0xFFFFFFFFu;
+}
+
+// byte form (qec_sample_depolarizing_dev): one lane per sample writes the bytes of its hit qubits
+// into rows the launcher zeroed
+__global__ __launch_bounds__(256) void sample_depolarizing_kernel(GapParams gp, uint64_t start, long long B, int n,
+                                                                  uint8_t* __restrict__ x, uint8_t* __restrict__ z)
+{
+    extern __shared__ uint32_t gap_T[];
+    gap_table(gp, n, gap_T);
+    __syncthreads();
+    const long long s = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= B || gp.thr == 0) return;
+    uint8_t* __restrict__ xr = x + s * n;
+    uint8_t* __restrict__ zr = z + s * n;
+    gap_walk(gp, start + (uint64_t)s, n, gap_T, [&](int v, uint32_t t) {
+        if (t != 2) xr[v] = 1;
+        if (t != 0) zr[v] = 1;
+    });
 }
 
 // counters, in qec_mc_counters order
@@ -176,7 +218,7 @@ __global__ __launch_bounds__(64 * kStatBlockWaves) void statistics_kernel(
     const int nw = (2 * n + 63) / 64;
     unsigned long long c[C_N + 2] = {};
     for (long long b = (long long)blockIdx.x * kStatBlockWaves + wv; b < B; b += (long long)gridDim.x * kStatBlockWaves) {
-        bool anyX = false, anyZ = false;
+        bool anyX = false, anyZ = false, anyR = false;  // anyR: wave-uniform (ballots)
         for (int w = 0; w < nw; ++w) {
             const int q = w * 64 + lane;
             bool bit = false;
@@ -190,15 +232,17 @@ __global__ __launch_bounds__(64 * kStatBlockWaves) void statistics_kernel(
                 bit = (ze ^ eZ[b * n + q - n]) & 1;
             }
             const unsigned long long word = __ballot(bit);
+            anyR |= word != 0ull;
             if (lane == 0) sres[wv][w] = word;
         }
-        wave_sync();
         const uint8_t f = flags[b];
         const bool dEX = f & QEC_SYNDROME_FAIL_X, dEZ = f & QEC_SYNDROME_FAIL_Z;
         bool logical = false;
-        if (!(dEX || dEZ) && imp_cw > 0)  // CheckLogicalError only when no syndrome failure
+        if (!(dEX || dEZ) && imp_cw > 0 && anyR) {  // CheckLogicalError only when no syndrome failure
+            wave_sync();
             logical = logical_from_columns<false>(sres[wv], nw, n, 0, imp_cols, imp_cw, lane);
-        wave_sync();  // sres is rewritten by the next sample
+            wave_sync();  // sres is rewritten by the next sample
+        }
         c[C_WITHX] += __any(anyX);
         c[C_WITHZ] += __any(anyZ);
         c[C_SYNX] += dEX;
@@ -237,7 +281,6 @@ __global__ void pack_decisions_kernel(const uint8_t* __restrict__ eX, const uint
 // ---- fused Monte-Carlo front end ----------------------------------------------------
 // One wave per sample, errors staged in LDS (this wave's x and z rows, each zero-padded to
 // npad = 8 nb bytes):
-//   source PHILOX: the depolarising sampler above, qubit by qubit (nothing read from HBM);
 //   source DRAWS:  the reference's W (index, type) draws of the sample (DecoderCPU.h:452-457);
 //   source BYTES:  x, z rows [B][n] from HBM.
 // Then, from LDS: the syndromes sX, sZ (QC: s(r, i) = XOR_l e[l P + (E[r][l] + i) mod P]; any other
@@ -248,8 +291,6 @@ constexpr int kMcWaves = 4;
 
 struct McArgs {
     // sources
-    Depol depol;                               // PHILOX
-    uint64_t start;
     const int32_t* idx;                        // DRAWS: [B][W] qubit indices
     const uint8_t* type;                       //        [B][W] 0 = X, 1 = Y, 2 = Z
     int W;
@@ -298,26 +339,6 @@ __global__ __launch_bounds__(64 * kMcWaves) void mc_errors_syndrome_kernel(const
             uint8_t* ex = stage + (size_t)sI * 2 * npad;
             if (ty == 0 || ty == 1) ex[v] = 1;  // several draws may hit one qubit: they all store 1
             if (ty == 2 || ty == 1) ex[npad + v] = 1;
-        }
-    } else if constexpr (SRC == MC_SRC_PHILOX) {
-        // four qubits per lane and Philox call, one 32-bit LDS word per row (npad is a multiple of
-        // 8, so the padding words are written too, zero past n)
-        const int ng = npad / 4;
-#pragma unroll 3
-        for (int t = lane; t < ns * ng; t += 64) {
-            const int sI = qdiv(t, a.magicG), g = t - sI * ng;
-            uint32_t x4 = 0, z4 = 0;
-            if (4 * g < n) {
-                depolarizing4(a.depol, a.start + (uint64_t)(b0 + sI), (uint32_t)g, x4, z4);
-                if (4 * g + 4 > n) {
-                    const uint32_t keep = 0xFFFFFFFFu >> (8 * (4 * g + 4 - n));
-                    x4 &= keep;
-                    z4 &= keep;
-                }
-            }
-            uint32_t* row = reinterpret_cast<uint32_t*>(stage + (size_t)sI * 2 * npad);
-            row[g] = x4;
-            row[ng + g] = z4;
         }
     } else {
         for (int t = lane; t < ns * npad; t += 64) {
@@ -403,13 +424,183 @@ __global__ __launch_bounds__(64 * kMcWaves) void mc_errors_syndrome_kernel(const
     }
 }
 
+// ---- fused front end for the depolarising sampler (the gap walk) ---------------------
+// One lane per sample: the lane walks its sample (gap_walk) and, for every hit, sets the qubit's
+// bits in the sample's packed-error words and flips the qubit's checks in its syndrome bit set
+// (both in LDS, this lane's own region: w32 = ew + sw words, errors in the decision-record layout,
+// then mX + mZ syndrome bits).  Then the wave writes its samples' contiguous output blocks (sX, sZ,
+// errp) as coalesced dwords (write_block).  QEC_GAP_WRITE = 0 has each lane write its own sample's
+// rows instead (write_row): 4x fewer instructions, but every store scatters over 64 rows, which
+// measured slower (P61, 65 536 samples at p = 0.002: 62 vs 41 us).  Nothing but syndromes and packed
+// errors reaches HBM, and the sampler costs words per hit, not per qubit.
+constexpr int kGapWaves = 4;
+
+struct GapArgs {
+    GapParams gp;
+    uint64_t start;
+    long long B;
+    int n, nb, mX, mZ, P, L, J, K;
+    int spw;           // samples per wave
+    int ew, w32;       // LDS words per sample: packed errors, then syndrome bits
+    uint32_t magicX, magicZ, magicE;  // ceil(2^32 / d) for d = mX, mZ, 2 nb
+    uint8_t* sX;
+    uint8_t* sZ;
+    uint8_t* errp;     // nullable
+    const int32_t* varEdge;  // non-QC codes: n x dvX then n x dvZ edge ids; check = edge / dc
+    int dc, dvX, dvZ;
+    int ablate;              // timing experiments only (QEC_GAP_ABLATE; wrong outputs): 1 no write-out, 2 no walk
+    int block_write;         // QEC_GAP_WRITE = 1: wave-block write-out (write_block)
+    int EX[128], EZ[128];    // QC codes
+};
+
+// Bytes [0, tot) of a wave's output block dst, byte k = f(k): head bytes up to 4-byte alignment,
+// then dwords, then the tail (dst is at any alignment).
+template <class F>
+__device__ __forceinline__ void write_block(uint8_t* __restrict__ dst, int tot, int lane, F&& f)
+{
+    const int head = min((int)((0u - (uint32_t)(uintptr_t)dst) & 3u), tot);
+    if (lane < head) dst[lane] = (uint8_t)f(lane);
+    const int body = (tot - head) >> 2;
+    uint32_t* __restrict__ d32 = reinterpret_cast<uint32_t*>(dst + head);
+#pragma unroll 4
+    for (int t = lane; t < body; t += 64) {
+        const int k = head + 4 * t;
+        d32[t] = f(k) | f(k + 1) << 8 | f(k + 2) << 16 | f(k + 3) << 24;
+    }
+    const int tail = head + 4 * body + lane;
+    if (tail < tot) dst[tail] = (uint8_t)f(tail);
+}
+
+// One lane's output row of len bytes at dst (any alignment): head bytes up to 4-byte alignment,
+// dwords, tail bytes; byte(c) = byte c, dword(c) = bytes c .. c+3 (little-endian).
+template <class Byte, class Dword>
+__device__ __forceinline__ void write_row(uint8_t* __restrict__ dst, int len, Byte&& byte, Dword&& dword)
+{
+    const int h = min((int)((0u - (uint32_t)(uintptr_t)dst) & 3u), len);
+    for (int c = 0; c < h; ++c) dst[c] = (uint8_t)byte(c);
+    const int nd = (len - h) >> 2;
+    uint32_t* __restrict__ d32 = reinterpret_cast<uint32_t*>(dst + h);
+    for (int t = 0; t < nd; ++t) d32[t] = dword(h + 4 * t);
+    for (int c = h + 4 * nd; c < len; ++c) dst[c] = (uint8_t)byte(c);
+}
+
+// bits c .. c+3 of a bit set (words w) as four 0/1 bytes
+__device__ __forceinline__ uint32_t bits4_to_bytes(const uint32_t* __restrict__ w, int c)
+{
+    const uint64_t pair = (uint64_t)w[c >> 5] | ((c & 31) > 28 ? (uint64_t)w[(c >> 5) + 1] << 32 : 0ull);
+    const uint32_t nib = (uint32_t)(pair >> (c & 31)) & 0xFu;
+    return (nib * 0x204081u) & 0x01010101u;  // nibble bit k -> byte k (the four shifted copies never overlap)
+}
+// bytes c .. c+3 of a byte string held in words w
+__device__ __forceinline__ uint32_t bytes4(const uint32_t* __restrict__ w, int c)
+{
+    const int sh = 8 * (c & 3);
+    const uint32_t lo = w[c >> 2];
+    return sh == 0 ? lo : (lo >> sh) | (w[(c >> 2) + 1] << (32 - sh));
+}
+
+__global__ __launch_bounds__(64 * kGapWaves) void mc_gap_kernel(const GapArgs a)
+{
+    extern __shared__ uint32_t gap_smem[];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int n = a.n;
+    uint32_t* __restrict__ T = gap_smem;                                            // [n + 1]
+    int* __restrict__ E = reinterpret_cast<int*>(gap_smem + n + 1);                 // [(J + K) L], QC
+    const int ne = a.varEdge ? 0 : (a.J + a.K) * a.L;
+    uint32_t* __restrict__ reg = gap_smem + n + 1 + ne + (size_t)wv * a.spw * a.w32;  // this wave's samples
+    gap_table(a.gp, n, T);
+    for (int t = threadIdx.x; t < ne; t += blockDim.x) E[t] = t < a.J * a.L ? a.EX[t] : a.EZ[t - a.J * a.L];
+    for (int t = lane; t < a.spw * a.w32; t += 64) reg[t] = 0u;
+    __syncthreads();
+    const long long b0 = ((long long)blockIdx.x * kGapWaves + wv) * a.spw;
+    if (b0 >= a.B) return;  // wave-local from here on
+    const int ns = (int)(a.B - b0 < a.spw ? a.B - b0 : a.spw);
+    if (lane < ns && a.gp.thr != 0 && a.ablate != 2) {
+        uint32_t* __restrict__ mine = reg + lane * a.w32;
+        uint32_t* __restrict__ syn = mine + a.ew;
+        const int zb = 8 * a.nb, P = a.P, L = a.L;
+        gap_walk(a.gp, a.start + (uint64_t)(b0 + lane), n, T, [&](int v, uint32_t t) {
+            const bool ex = t != 2, ez = t != 0;
+            if (ex) atomicOr(&mine[v >> 5], 1u << (v & 31));
+            if (ez) atomicOr(&mine[(zb + v) >> 5], 1u << ((zb + v) & 31));
+            if (a.varEdge == nullptr) {
+                // QC: qubit (l, j) sits in check (r, (j - E[r][l]) mod P) of each block row r
+                const int l = v / P, j = v - l * P;
+                if (ex)
+                    for (int r = 0; r < a.J; ++r) {
+                        const int d = j - E[r * L + l];
+                        const int c = r * P + (d < 0 ? d + P : d);
+                        atomicXor(&syn[c >> 5], 1u << (c & 31));
+                    }
+                if (ez)
+                    for (int r = 0; r < a.K; ++r) {
+                        const int d = j - E[(a.J + r) * L + l];
+                        const int c = a.mX + r * P + (d < 0 ? d + P : d);
+                        atomicXor(&syn[c >> 5], 1u << (c & 31));
+                    }
+            } else {
+                if (ex)
+                    for (int k = 0; k < a.dvX; ++k) {
+                        const int c = a.varEdge[(size_t)v * a.dvX + k] / a.dc;
+                        atomicXor(&syn[c >> 5], 1u << (c & 31));
+                    }
+                if (ez)
+                    for (int k = 0; k < a.dvZ; ++k) {
+                        const int c = a.varEdge[(size_t)n * a.dvX + (size_t)v * a.dvZ + k] / a.dc;  // Z ids are offset by mX dc
+                        atomicXor(&syn[c >> 5], 1u << (c & 31));
+                    }
+            }
+        });
+    }
+    wave_sync();
+    if (a.ablate == 1) return;
+    const int w32 = a.w32, ew = a.ew;
+    if (!a.block_write) {
+        if (lane < ns) {
+            const long long b = b0 + lane;
+            const uint32_t* __restrict__ mine = reg + lane * w32;
+            const uint32_t* __restrict__ syn = mine + ew;
+            write_row(a.sX + b * a.mX, a.mX, [&](int c) { return (syn[c >> 5] >> (c & 31)) & 1u; },
+                      [&](int c) { return bits4_to_bytes(syn, c); });
+            write_row(a.sZ + b * a.mZ, a.mZ, [&](int c) { return (syn[(a.mX + c) >> 5] >> ((a.mX + c) & 31)) & 1u; },
+                      [&](int c) { return bits4_to_bytes(syn, a.mX + c); });
+            if (a.errp != nullptr) {
+                const int eb = 2 * a.nb;
+                write_row(a.errp + b * eb, eb, [&](int c) { return (mine[c >> 2] >> (8 * (c & 3))) & 0xFFu; },
+                          [&](int c) { return bytes4(mine, c); });
+            }
+        }
+        return;
+    }
+    write_block(a.sX + b0 * a.mX, ns * a.mX, lane, [&](int k) -> uint32_t {
+        const int s = qdiv(k, a.magicX), c = k - s * a.mX;
+        return (reg[s * w32 + ew + (c >> 5)] >> (c & 31)) & 1u;
+    });
+    write_block(a.sZ + b0 * a.mZ, ns * a.mZ, lane, [&](int k) -> uint32_t {
+        const int s = qdiv(k, a.magicZ), c = a.mX + (k - s * a.mZ);
+        return (reg[s * w32 + ew + (c >> 5)] >> (c & 31)) & 1u;
+    });
+    if (a.errp != nullptr) {
+        const int eb = 2 * a.nb;
+        write_block(a.errp + b0 * eb, ns * eb, lane, [&](int k) -> uint32_t {
+            const int s = qdiv(k, a.magicE), c = k - s * eb;
+            return (reg[s * w32 + (c >> 2)] >> (8 * (c & 3))) & 0xFFu;
+        });
+    }
+}
+
 // CodeStatistics counters of a batch from bit-packed errors errp [B][2 nb] and decision records
 // rec [B][2 nb + 1] (qec_decode_batch_packed_dev): the residual [x ^ eX | z ^ eZ] is their XOR
 // over the first 2 nb bytes (record layout), tested by logical_from_columns; optional iteration
 // sums (iters [B][2]) into counters[8], counters[9].
-// One wave per sample; counters as statistics_kernel (DecoderCPU.h:464-521).
+// One wave per sample; counters as statistics_kernel (DecoderCPU.h:464-521).  A wave takes U
+// samples at a time and issues all their byte loads (NJ per lane and sample) before using any, so
+// one memory latency covers U samples; the residual is staged in LDS only for the rare sample that
+// needs the I-P columns (no syndrome failure, nonzero residual).  NJ = 0: any code, one sample at
+// a time.
 constexpr int kMaxRecWords = 80;  // 2 nb <= 640 bytes
 
+template <int NJ, int U>
 __global__ __launch_bounds__(64 * kStatBlockWaves) void statistics_packed_kernel(
     const uint8_t* __restrict__ errp, const uint8_t* __restrict__ rec, const int32_t* __restrict__ iters, long long B,
     int n, int nb, const uint64_t* __restrict__ imp_cols, int imp_cw, unsigned long long* __restrict__ counters)
@@ -419,37 +610,60 @@ __global__ __launch_bounds__(64 * kStatBlockWaves) void statistics_packed_kernel
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int recB = 2 * nb + 1;
     const int nw = (2 * nb + 7) / 8;
+    const int nj = NJ > 0 ? NJ : (8 * nw + 63) / 64;
     unsigned long long c[C_N + 2] = {};
-    for (long long b = (long long)blockIdx.x * kStatBlockWaves + wv; b < B; b += (long long)gridDim.x * kStatBlockWaves) {
-        bool anyX = false, anyZ = false;
-        for (int t = lane; t < 8 * nw; t += 64) {
-            uint8_t r = 0;
-            if (t < 2 * nb) {
-                const uint8_t e = errp[b * 2 * nb + t];
-                if (t < nb) anyX |= e != 0; else anyZ |= e != 0;
-                r = e ^ rec[b * recB + t];
+    const long long step = (long long)gridDim.x * kStatBlockWaves * U;
+    for (long long b0 = ((long long)blockIdx.x * kStatBlockWaves + wv) * U; b0 < B; b0 += step) {
+        uint32_t any[U];  // per lane and sample: bit 0 x errors, bit 1 z errors, bit 2 residual
+        uint8_t f[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const long long b = b0 + u;
+            any[u] = 0;
+            f[u] = 0;
+            if (b < B) {
+                f[u] = rec[b * recB + 2 * nb];
+#pragma unroll
+                for (int j = 0; j < (NJ > 0 ? NJ : 1); ++j) {
+                    for (int jj = j; jj < (NJ > 0 ? j + 1 : nj); ++jj) {
+                        const int t = lane + 64 * jj;
+                        if (t < 2 * nb) {
+                            const uint8_t e = errp[b * 2 * nb + t];
+                            const uint8_t r = e ^ rec[b * recB + t];
+                            any[u] |= (e != 0 ? (t < nb ? 1u : 2u) : 0u) | (r != 0 ? 4u : 0u);
+                        }
+                    }
+                }
             }
-            sres[wv][t] = r;
         }
-        wave_sync();
-        const uint8_t f = rec[b * recB + 2 * nb];
-        const bool dEX = f & QEC_SYNDROME_FAIL_X, dEZ = f & QEC_SYNDROME_FAIL_Z;
-        bool logical = false;
-        if (!(dEX || dEZ) && imp_cw > 0)  // CheckLogicalError only when no syndrome failure
-            logical = logical_from_columns<true>(reinterpret_cast<const unsigned long long*>(sres[wv]), nw, n, nb,
-                                                 imp_cols, imp_cw, lane);
-        wave_sync();
-        c[C_WITHX] += __any(anyX);
-        c[C_WITHZ] += __any(anyZ);
-        c[C_SYNX] += dEX;
-        c[C_SYNZ] += dEZ;
-        c[C_LOGICAL] += !(dEX || dEZ) && logical;
-        c[C_CORRECTED] += !(dEX || dEZ) && !logical;
-        c[C_CONVX] += (f & QEC_CONVERGENCE_FAIL_X) != 0;
-        c[C_CONVZ] += (f & QEC_CONVERGENCE_FAIL_Z) != 0;
-        if (iters != nullptr) {
-            c[C_N] += (unsigned)iters[2 * b];
-            c[C_N + 1] += (unsigned)iters[2 * b + 1];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const long long b = b0 + u;
+            if (b >= B) break;
+            const bool dEX = f[u] & QEC_SYNDROME_FAIL_X, dEZ = f[u] & QEC_SYNDROME_FAIL_Z;
+            bool logical = false;
+            // CheckLogicalError only when no syndrome failure; a zero residual (the decoder found the
+            // error itself, the common case) has (I-P) r = 0 without reading a column
+            if (!(dEX || dEZ) && imp_cw > 0 && __any(any[u] & 4u)) {
+                for (int t = lane; t < 8 * nw; t += 64)
+                    sres[wv][t] = t < 2 * nb ? (uint8_t)(errp[b * 2 * nb + t] ^ rec[b * recB + t]) : (uint8_t)0;
+                wave_sync();
+                logical = logical_from_columns<true>(reinterpret_cast<const unsigned long long*>(sres[wv]), nw, n, nb,
+                                                     imp_cols, imp_cw, lane);
+                wave_sync();
+            }
+            c[C_WITHX] += __any(any[u] & 1u);
+            c[C_WITHZ] += __any(any[u] & 2u);
+            c[C_SYNX] += dEX;
+            c[C_SYNZ] += dEZ;
+            c[C_LOGICAL] += !(dEX || dEZ) && logical;
+            c[C_CORRECTED] += !(dEX || dEZ) && !logical;
+            c[C_CONVX] += (f[u] & QEC_CONVERGENCE_FAIL_X) != 0;
+            c[C_CONVZ] += (f[u] & QEC_CONVERGENCE_FAIL_Z) != 0;
+            if (iters != nullptr) {
+                c[C_N] += (unsigned)iters[2 * b];
+                c[C_N + 1] += (unsigned)iters[2 * b + 1];
+            }
         }
     }
     stat_flush(part, c, iters != nullptr ? C_N + 2 : C_N, counters);
@@ -467,19 +681,71 @@ int launch_sample_depolarizing(uint64_t seed, uint64_t start, long long B, int n
                                hipStream_t st)
 {
     if (B <= 0) return QEC_OK;
-    const long long tot = B * ((n + 3) / 4);
-    hipLaunchKernelGGL(sample_depolarizing_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st,
-                       make_depol(seed, p), start, B, n, x, z);
+    if (hipMemsetAsync(x, 0, (size_t)B * n, st) != hipSuccess || hipMemsetAsync(z, 0, (size_t)B * n, st) != hipSuccess)
+        return fail(QEC_ERR_HIP, "sample_depolarizing: memset failed");
+    hipLaunchKernelGGL(sample_depolarizing_kernel, dim3((unsigned)((B + 255) / 256)), dim3(256),
+                       (size_t)(n + 1) * sizeof(uint32_t), st, make_gap(seed, p), start, B, n, x, z);
     return launch_check("sample_depolarizing");
+}
+
+static uint32_t magic_of(long long d) { return d > 1 ? (uint32_t)(((1ull << 32) + (uint64_t)d - 1) / (uint64_t)d) : 0u; }
+
+// samples per wave of mc_gap_kernel (QEC_GAP_SPW overrides, for experiments)
+static int gap_spw_default()
+{
+    static const int v = [] {
+        const char* e = std::getenv("QEC_GAP_SPW");
+        const int k = e ? std::atoi(e) : 0;
+        return k >= 1 && k <= 64 ? k : 16;
+    }();
+    return v;
+}
+
+static int launch_mc_gap(const McArgsHost& h, hipStream_t st)
+{
+    const Code& c = *h.code;
+    GapArgs a{};
+    a.gp = make_gap(h.seed, h.p);
+    a.start = h.start;
+    a.B = h.B;
+    a.n = c.n; a.nb = (c.n + 7) / 8; a.mX = c.mX; a.mZ = c.mZ; a.P = c.P; a.L = c.L; a.J = c.J; a.K = c.K;
+    a.sX = h.sX; a.sZ = h.sZ; a.errp = h.errp;
+    a.varEdge = h.varEdge;
+    a.dc = c.L; a.dvX = c.J; a.dvZ = c.K;
+    {
+        static const int ab = [] { const char* e = std::getenv("QEC_GAP_ABLATE"); return e ? std::atoi(e) : 0; }();
+        a.ablate = ab;
+        static const int bw = [] { const char* e = std::getenv("QEC_GAP_WRITE"); return e ? std::atoi(e) : 1; }();
+        a.block_write = bw;
+    }
+    if (a.varEdge == nullptr) {
+        if (!c.is_qc || c.J * c.L > 128 || c.K * c.L > 128)
+            return fail(QEC_ERR_UNSUPPORTED, "mc front end: needs a QC code or a check table");
+        for (size_t k = 0; k < c.EX.size(); ++k) a.EX[k] = c.EX[k];
+        for (size_t k = 0; k < c.EZ.size(); ++k) a.EZ[k] = c.EZ[k];
+    }
+    a.ew = (2 * a.nb + 3) / 4;
+    a.w32 = a.ew + (c.mX + c.mZ + 31) / 32;
+    // at most 16 KiB of sample state per wave
+    a.spw = std::max(1, std::min(gap_spw_default(), 16384 / (4 * a.w32)));
+    if ((long long)a.spw * std::max<long long>({(long long)c.mX, (long long)c.mZ, 2LL * a.nb}) >= 65536)
+        return fail(QEC_ERR_UNSUPPORTED, "mc front end: code too long");
+    a.magicX = magic_of(c.mX); a.magicZ = magic_of(c.mZ); a.magicE = magic_of(2 * a.nb);
+    const int ne = a.varEdge ? 0 : (c.J + c.K) * c.L;
+    const size_t smem = 4 * ((size_t)c.n + 1 + ne + (size_t)kGapWaves * a.spw * a.w32);
+    if (smem > 64 * 1024) return fail(QEC_ERR_UNSUPPORTED, "mc front end: code too long for the LDS stage");
+    const long long per_block = (long long)kGapWaves * a.spw;
+    hipLaunchKernelGGL(mc_gap_kernel, dim3((unsigned)((h.B + per_block - 1) / per_block)), dim3(64 * kGapWaves), smem,
+                       st, a);
+    return launch_check("mc_gap");
 }
 
 int launch_mc_errors_syndrome(int src, const McArgsHost& h, hipStream_t st)
 {
     if (h.B <= 0) return QEC_OK;
+    if (src == MC_SRC_PHILOX) return launch_mc_gap(h, st);
     const Code& c = *h.code;
     McArgs a{};
-    a.depol = make_depol(h.seed, h.p);
-    a.start = h.start;
     a.idx = h.idx; a.type = h.type; a.W = h.W;
     a.x = h.x; a.z = h.z;
     a.sX = h.sX; a.sZ = h.sZ; a.errp = h.errp;
@@ -509,9 +775,7 @@ int launch_mc_errors_syndrome(int src, const McArgsHost& h, hipStream_t st)
 #define QEC_MC_LAUNCH(S)                                                              \
     (lt == 10 ? launch(mc_errors_syndrome_kernel<S, 10>)                              \
               : lt == 6 ? launch(mc_errors_syndrome_kernel<S, 6>) : launch(mc_errors_syndrome_kernel<S, 0>))
-    if (src == MC_SRC_PHILOX)
-        QEC_MC_LAUNCH(MC_SRC_PHILOX);
-    else if (src == MC_SRC_DRAWS)
+    if (src == MC_SRC_DRAWS)
         QEC_MC_LAUNCH(MC_SRC_DRAWS);
     else
         QEC_MC_LAUNCH(MC_SRC_BYTES);
@@ -526,9 +790,12 @@ int launch_statistics_packed(const Code& c, const uint64_t* imp_cols, const uint
     const int nb = (c.n + 7) / 8;
     if ((2 * nb + 7) / 8 > kMaxRecWords || c.imp_col_words > 64)
         return fail(QEC_ERR_UNSUPPORTED, "packed statistics kernel: code too long");
-    const long long blocks = std::min<long long>((B + kStatBlockWaves - 1) / kStatBlockWaves, kStatMaxBlocks);
-    hipLaunchKernelGGL(statistics_packed_kernel, dim3((unsigned)blocks), dim3(64 * kStatBlockWaves), 0, st, errp, rec,
-                       iters, B, c.n, nb, imp_cols, c.imp_col_words, counters);
+    const int nj = (8 * ((2 * nb + 7) / 8) + 63) / 64;
+    constexpr int U = 4;
+    const long long blocks = std::min<long long>((B + kStatBlockWaves * U - 1) / (kStatBlockWaves * U), kStatMaxBlocks);
+    auto kern = nj == 1 ? statistics_packed_kernel<1, U> : nj == 3 ? statistics_packed_kernel<3, U> : statistics_packed_kernel<0, 1>;
+    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(64 * kStatBlockWaves), 0, st, errp, rec, iters, B, c.n, nb,
+                       imp_cols, c.imp_col_words, counters);
     return launch_check("statistics_packed");
 }
 

@@ -58,7 +58,8 @@ struct Mt19937 {
 };
 
 // Host description of a fused Monte-Carlo front-end launch (montecarlo.hip,
-// mc_errors_syndrome_kernel): error source (MC_SRC_*), syndromes out, packed errors out.
+// mc_errors_syndrome_kernel, or mc_gap_kernel for PHILOX): error source (MC_SRC_*), syndromes out,
+// packed errors out.
 enum { MC_SRC_PHILOX = 0, MC_SRC_DRAWS = 1, MC_SRC_BYTES = 2 };
 struct McArgsHost {
     const Code* code = nullptr;
@@ -72,7 +73,8 @@ struct McArgsHost {
     uint8_t* sX = nullptr;
     uint8_t* sZ = nullptr;
     uint8_t* errp = nullptr;        // [B][2 ceil(n/8)], nullable
-    const int32_t* chkVar = nullptr;
+    const int32_t* chkVar = nullptr;  // non-QC codes: check -> variables (BYTES, DRAWS)
+    const int32_t* varEdge = nullptr; // non-QC codes: variable -> edges (PHILOX, the gap walk)
     long long B = 0;
 };
 

@@ -9,7 +9,7 @@ at every N).  `--batch` instead fixes the per-GPU batch (weak scaling), labelled
 One step = one batched decode of the rank's resident shard (both sectors, reference update
 rules, exactly `--iters` iterations) writing bit-packed decision records (eX bits, eZ bits,
 flags byte: SURVEY.md 8(d)'s I/O model).  Syndromes are generated on the device (fused
-Philox sampler + syndrome kernel) before the timed region.  There is no collective in the
+gap-walk sampler + syndrome kernel) before the timed region.  There is no collective in the
 decode step (syndromes are independent); at N > 1 the RCCL gather of every rank's records to
 rank 0 is timed separately, as its own component and end to end (decode + gather per step).
 
@@ -162,7 +162,7 @@ def main():
         dec.set_option(k, int(v))
 
     # the rank's shard of the sample index space, drawn and turned into syndromes on the device
-    # (fused Philox sampler + syndrome kernel) before the timed region
+    # (fused gap-walk sampler + syndrome kernel) before the timed region
     sX = torch.empty((B, code.numEqsX), dtype=torch.uint8, device=dev)
     sZ = torch.empty((B, code.numEqsZ), dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream(dev)
@@ -230,7 +230,7 @@ def main():
         "scaling": scaling,
         "vs_baseline": None,
         "dtype": "f32",
-        "data": "synthetic i.i.d. depolarising errors (device Philox4x32-10 sampler, seed 0x51EC0DE), "
+        "data": "synthetic i.i.d. depolarising errors (device gap-walk sampler over Philox4x32-10, seed 0x51EC0DE), "
                 "syndromes resident in HBM",
         "config": {"workload": workload + ", " + stop_label, "code": code.describe(), "global_batch": global_batch,
                    "per_gpu_batch": B, "bp_iters": iters, "stop": args.stop, "p": p, "output": args.output,

@@ -241,11 +241,13 @@ typedef struct {
 } qec_mc_result;
 
 /* i.i.d. depolarising errors for samples [start, start+B) of stream `seed` (device buffers
- * x, z: B x n).  Philox4x32-10, one call per four qubits: qubits 4g..4g+3 of sample b use counter
- * (b lo, b hi, g, 0x51EC0DE5) and key (seed lo, seed hi), output word j for qubit 4g + j.  The
- * qubit is hit if w < thr = floor(p 2^32) (saturated); its type is floor(w mul / 2^64) with
- * mul = min(floor(3 2^64 / thr), 2^64 - 1): 0 = X, 1 = Y, 2 = Z (each 1/3 to within 1/thr; Y sets
- * both bits).  Any shard of the index space can be drawn alone. */
+ * x, z: B x n).  Each qubit is hit with probability thr / 2^32, thr = floor(p 2^32) (saturated),
+ * independently, drawn as a walk over the gaps between hits: sample b reads 32-bit words from
+ * Philox4x32-10 calls k = 0, 1, ... (counter (b lo, b hi, k, 0x6A9C0DE5), key (seed lo, seed hi),
+ * word 4k + j = output word j of call k); u = next word skips G = #{g in 1..n : u < T[g]} qubits,
+ * T[g] = floor(q^g 2^32), q = 1 - thr / 2^32 (q^g by right-to-left binary exponentiation in IEEE
+ * double); a qubit still inside the sample is then hit, of type floor(3 w / 2^32) of the next word
+ * w: 0 = X, 1 = Y, 2 = Z (Y sets both bits).  Any shard of the index space can be drawn alone. */
 int qec_sample_depolarizing_dev(qec_decoder* dec, uint64_t seed, uint64_t start, size_t B, float p, uint8_t* x,
                                 uint8_t* z, void* stream);
 /* Fused front end: the depolarising errors of qec_sample_depolarizing_dev (same stream, same

@@ -422,7 +422,8 @@ class DecoderGPU:
                "qec_decode_batch_packed_dev")
 
     def sample_depolarizing_dev(self, seed, start, p, x, z, stream=None):
-        """Device Philox depolarising errors for samples [start, start + x.shape[0])."""
+        """Device depolarising errors (the gap walk over Philox4x32-10 words, include/qec_ldpc.h)
+        for samples [start, start + x.shape[0])."""
         import torch
         self._single("sample_depolarizing_dev")
         B, n = x.shape[0], self.code.n

@@ -125,6 +125,14 @@ namespace qec {
 #ifndef QEC_SYN_ROWBARRIER
 #define QEC_SYN_ROWBARRIER 1
 #endif
+//   QEC_AGREE_SYN    the syndrome-stop kernels take the agreement test too (kAgree)
+#ifndef QEC_AGREE_SYN
+#define QEC_AGREE_SYN 0
+#endif
+//   QEC_SYN_RELAUNDER   the syndrome test recomputes its rotation addresses (see iteration)
+#ifndef QEC_SYN_RELAUNDER
+#define QEC_SYN_RELAUNDER 1
+#endif
 //   QEC_COL_GROUP    columns per division guard in soft var passes (var_pass); 0: per variant
 #ifndef QEC_COL_GROUP
 #define QEC_COL_GROUP 0
@@ -856,6 +864,17 @@ __device__ __forceinline__ bool lane_syndrome_ok(const BpArgs& a, uint32_t hdmas
     return match;
 }
 
+// Whether a hard sector first tries the whole-sector agreement test (var_pass_agree, the entry to
+// the cycle jump).  Not for the syndrome stop rule: there it costs more than it saves -- with it the
+// P61 kernel spills at 128 VGPRs, without it P61 decodes 4-15 % faster at p = 0.1 .. 0.002 and P7
+// 7 % (tools/gpu/run_syn_variants.sh, profiles/r02/syn_variants_r02s3h.txt); sectors that never
+// satisfy their syndrome then run their hard iterations instead of jumping (same outputs).
+template <int STOP>
+constexpr bool kAgree()
+{
+    return QEC_AGREE && (STOP != QEC_STOP_SYNDROME || QEC_AGREE_SYN);
+}
+
 // One BP iteration; returns true if this group stops after it.
 // hard: every variable->check message of this sector is exactly +0 or 1.0 (wave-uniform).
 // agreed: set when the iteration took the agreement path (hard sector, every variable's inputs
@@ -877,7 +896,7 @@ __device__ __forceinline__ bool iteration(const BpArgs& a, float (&msg)[R][L], u
     vagree = false;
     if (TU::kSaturate && hard) {
         check_pass_hard<R, L>(msg, sbits);  // outputs are hard too: hard stays set for the var pass
-        agreed = QEC_AGREE && (LAST || R >= 2) && var_pass_agree<R, L, SEC, HD, SH>(a, msg, ln, hdmask);
+        agreed = kAgree<STOP>() && (LAST || R >= 2) && var_pass_agree<R, L, SEC, HD, SH>(a, msg, ln, hdmask);
         if (agreed)
             vagree = true;
         else
@@ -898,6 +917,9 @@ __device__ __forceinline__ bool iteration(const BpArgs& a, float (&msg)[R][L], u
         if (n % 10 == 0) return group_all_sh<SH>(lane_converged<R, L>(msg), ln, P);  // DecoderCPU.h:287-290
     } else if constexpr (STOP == QEC_STOP_SYNDROME) {
         hd_out = hdmask;  // the hard decision of the new state (what the post-processing would compute)
+        // launder the bases again: the test's rotations are var_pass's return rotations, whose
+        // addresses would otherwise be kept live across the whole var pass for reuse here
+        if constexpr (SH::kMaskSelect && QEC_SYN_RELAUNDER) asm volatile("" : "+v"(ln.b0), "+v"(ln.b1));
         return group_all_sh<SH>(lane_syndrome_ok<R, L, SEC, SH>(a, hdmask, sbits, ln), ln, P);
     }
     return false;
@@ -1332,7 +1354,7 @@ using KernelFn = void (*)(const BpArgs);
 using TuneP61 = Tune<5, true, false, true, true, false, true, 1, 2, 4>;
 struct TuneP61MinReg : TuneP61 {};
 using ShiftsP61 = GeneratedShifts<4, 5, 10, 61, 9, 49, TuneP61::kRelabel, TuneP61::kMaskSelect>;
-using TuneP7 = Tune<8, false, false, true, true, true>;
+using TuneP7 = Tune<8, false, false, true, true, true, false, 0, 4, 6>;
 struct TuneP7MinReg : TuneP7 {};
 using ShiftsP7 = GeneratedShifts<3, 3, 6, 7, 2, 3, TuneP7::kRelabel, TuneP7::kMaskSelect>;
 #ifndef QEC_P61_MINREG
@@ -1433,7 +1455,10 @@ static Variant gen()
 // takes the short division again (0.090 vs 0.092 ms, cmp_s6j).  P61 then moves to 5 waves per
 // SIMD (96 VGPRs, a few spills) and 2-wave workgroups: fixed stop 0.728 vs 0.751 ms at p = 0.01,
 // 1.75 vs 2.16 ms at p = 0.05; its syndrome-stop kernels spill badly at 5 waves (450 scratch
-// loads, 1.01 vs 0.50 ms) and keep 4 (profiles/r01/session7/cmp_s7l-n_*.txt).
+// loads, 1.01 vs 0.50 ms) and keep 4 (profiles/r01/session7/cmp_s7l-n_*.txt).  Round 2: without
+// the agreement test (kAgree) the syndrome-stop kernels are spill-free, P61 at 4 waves (125 VGPRs)
+// and P7 at 6 (75 VGPRs; as fast as 7 waves with 9 spills and 1-4 % faster than 8 with 40-70,
+// profiles/r02/syn_variants_r02s3i.txt).
 static Variant gen_p61()
 {
     Variant v = gen<4, 5, 10, 61, 9, 49, TuneP61>();

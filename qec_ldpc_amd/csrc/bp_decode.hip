@@ -191,8 +191,9 @@ constexpr int kMaxR = 16;
 constexpr int kMaxL = 32;
 
 struct BpArgs {
-    const uint8_t* sX;
+    const uint8_t* sX;  // [B][mX] bytes, or with sbits set [B][wX] words of bits (bit c = check c)
     const uint8_t* sZ;
+    int sbits, wX, wZ;
     uint8_t* eX;
     uint8_t* eZ;
     uint8_t* flags;
@@ -1032,9 +1033,18 @@ __device__ __forceinline__ uint32_t load_sbits(const BpArgs& a, const Lane& ln, 
     const uint8_t* __restrict__ s = SEC ? a.sZ : a.sX;
     uint32_t sbits = 0;
     if (in_range) {
+        if (a.sbits) {  // bit rows (the Monte-Carlo pipeline's layout)
+            const uint32_t* __restrict__ w = reinterpret_cast<const uint32_t*>(s) + (size_t)b * (SEC ? a.wZ : a.wX);
 #pragma unroll
-        for (int r = 0; r < R; ++r)
-            sbits |= (uint32_t)(s[(size_t)b * m + r * P + wrap(ln.i + SH::template rowoff<SEC>(a, r), P)] & 1) << r;
+            for (int r = 0; r < R; ++r) {
+                const int c = r * P + wrap(ln.i + SH::template rowoff<SEC>(a, r), P);
+                sbits |= ((w[c >> 5] >> (c & 31)) & 1u) << r;
+            }
+        } else {
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+                sbits |= (uint32_t)(s[(size_t)b * m + r * P + wrap(ln.i + SH::template rowoff<SEC>(a, r), P)] & 1) << r;
+        }
     }
     return sbits;
 }
@@ -1537,7 +1547,7 @@ bool decode_has_phase_stats(const void* variant, int stop)
     return static_cast<const Variant*>(variant)->phase[stop] != nullptr;
 }
 
-int launch_decode(const void* variant, const Code& c, const uint8_t* sX, const uint8_t* sZ, long long B,
+int launch_decode(const void* variant, const Code& c, const uint8_t* sX, const uint8_t* sZ, bool sbits, long long B,
                   float errorProbability, int maxIter, int stop, uint8_t* eX, uint8_t* eZ, uint8_t* flags,
                   uint8_t* rec, int32_t* iters, float* q, int hardPaths, const int32_t* perm, int split,
                   uint32_t* merge, bool merge_zeroed, hipStream_t stream)
@@ -1547,6 +1557,9 @@ int launch_decode(const void* variant, const Code& c, const uint8_t* sX, const u
     if (B >= (1LL << 31)) return fail(QEC_ERR_ARG, "bp_decode: at most 2^31 - 1 syndromes per launch");
     BpArgs a{};
     a.sX = sX; a.sZ = sZ; a.eX = eX; a.eZ = eZ; a.flags = flags; a.iters = iters; a.q = q;
+    a.sbits = sbits ? 1 : 0;
+    a.wX = (c.mX + 31) / 32;
+    a.wZ = (c.mZ + 31) / 32;
     a.rec = rec;
     a.perm = perm;
     const bool phase = (hardPaths & QEC_HP_PHASE) != 0;

@@ -15,20 +15,20 @@
 namespace qec {
 const char* last_error_cstr();
 const void* select_variant(const Code& c, std::string& name);
-int launch_decode(const void* variant, const Code& c, const uint8_t* sX, const uint8_t* sZ, long long B,
+int launch_decode(const void* variant, const Code& c, const uint8_t* sX, const uint8_t* sZ, bool sbits, long long B,
                   float errorProbability, int maxIter, int stop, uint8_t* eX, uint8_t* eZ, uint8_t* flags,
                   uint8_t* rec, int32_t* iters, float* q, int hardPaths, const int32_t* perm, int split,
                   uint32_t* merge, bool merge_zeroed, hipStream_t stream);
 size_t schedule_workspace_bytes(long long B, int mX, int mZ);
 long long schedule_max_batch();
-int launch_schedule(const uint8_t* sX, const uint8_t* sZ, long long B, int mX, int mZ, void* ws,
+int launch_schedule(const uint8_t* sX, const uint8_t* sZ, bool sbits, long long B, int mX, int mZ, void* ws,
                     uint32_t* zero_merge, int32_t** perm_out, hipStream_t st);
 bool decode_uses_split(const void* variant, int stop, int split);
 bool decode_has_phase_stats(const void* variant, int stop);
 int launch_sample_depolarizing(uint64_t seed, uint64_t start, long long B, int n, float p, uint8_t* x, uint8_t* z,
                                hipStream_t st);
 int launch_mc_errors_syndrome(int src, const McArgsHost& h, hipStream_t st);
-int launch_statistics_packed(const Code& c, const uint64_t* imp_cols, const uint8_t* errp, const uint8_t* rec,
+int launch_statistics_packed(const Code& c, const uint64_t* imp_cols, const uint8_t* errp, int estride, const uint8_t* rec,
                              const int32_t* iters, long long B, unsigned long long* counters, hipStream_t st);
 void* sparse_plan_create(const Code& c, int device);
 void sparse_plan_free(void* plan);
@@ -458,14 +458,18 @@ constexpr long long kScheduleMaxSingle = 1LL << 19;
 
 // One decode launch of a single-device handle on device buffers.  Outputs: byte form (eX, eZ,
 // flags) or, with rec non-null, the packed decision records.
+// sbits: sX / sZ are bit rows ([B][ceil(m/32)] words, the Monte-Carlo pipeline's layout; wave-circulant
+// engine only), else byte rows
 int dispatch_decode(qec_decoder* d, const uint8_t* sX, const uint8_t* sZ, long long B, float p, int maxIter, int stop,
-                    uint8_t* eX, uint8_t* eZ, uint8_t* flags, uint8_t* rec, int32_t* iters, float* q, hipStream_t st)
+                    uint8_t* eX, uint8_t* eZ, uint8_t* flags, uint8_t* rec, int32_t* iters, float* q, hipStream_t st,
+                    bool sbits = false)
 {
     if (B <= 0) return QEC_OK;
     const Code& c = *d->code;
     int rc = ws_acquire(d, st);
     if (rc) return rc;
     if (d->engine == QEC_ENGINE_SPARSE) {
+        if (sbits) return fail(QEC_ERR_UNSUPPORTED, "decode: bit-row syndromes need the wave-circulant engine");
         if (rec != nullptr) {  // byte outputs into the handle's staging, then packed
             if ((rc = ws_reserve(d->eX, (size_t)B * c.n, st, "decode")) || (rc = ws_reserve(d->eZ, (size_t)B * c.n, st, "decode")) ||
                 (rc = ws_reserve(d->flags, (size_t)B, st, "decode")))
@@ -490,12 +494,12 @@ int dispatch_decode(qec_decoder* d, const uint8_t* sX, const uint8_t* sZ, long l
             return rc;
         int32_t* pm = nullptr;
         // a sector-split launch merges its flags in zeroed words: the order pass zeroes them
-        rc = launch_schedule(sX, sZ, B, c.mX, c.mZ, d->sched.data(), split ? d->merge.data() : nullptr, &pm, st);
+        rc = launch_schedule(sX, sZ, sbits, B, c.mX, c.mZ, d->sched.data(), split ? d->merge.data() : nullptr, &pm, st);
         if (rc) return rc;
         perm = pm;
         zeroed = split;
     }
-    rc = launch_decode(d->variant, c, sX, sZ, B, p, maxIter, stop, eX, eZ, flags, rec, iters, q, hp, perm,
+    rc = launch_decode(d->variant, c, sX, sZ, sbits, B, p, maxIter, stop, eX, eZ, flags, rec, iters, q, hp, perm,
                        d->sector_split, split ? d->merge.data() : nullptr, zeroed, st);
     if (rc) return rc;
     return ws_release(d, st);
@@ -669,8 +673,10 @@ int mc_reserve(qec_decoder* d, size_t B, int W)
     const Code& c = *d->code;
     const size_t nb = (size_t)(c.n + 7) / 8;
     try {
-        d->msX.reserve(B * c.mX); d->msZ.reserve(B * c.mZ);
-        d->merrp.reserve(B * 2 * nb); d->mrec.reserve(B * (2 * nb + 1));
+        // syndromes as bytes or as bit rows, packed errors at 2 nb or word-aligned rows (mc_batch)
+        d->msX.reserve(B * std::max<size_t>(c.mX, 4 * ((c.mX + 31) / 32)));
+        d->msZ.reserve(B * std::max<size_t>(c.mZ, 4 * ((c.mZ + 31) / 32)));
+        d->merrp.reserve(B * 4 * ((2 * nb + 3) / 4)); d->mrec.reserve(B * (2 * nb + 1));
         d->mit.reserve(2 * B);
         if (W > 0) { d->midx.reserve(B * W); d->mtype.reserve(B * W); }
     } catch (const std::exception& ex) {
@@ -685,19 +691,31 @@ int mc_batch(qec_decoder* d, McArgsHost h, int src, float p, int maxIter, int st
              hipEvent_t ev0, hipEvent_t ev1)
 {
     hipStream_t st = d->stream;
-    h.code = d->code.get();
-    h.sX = d->msX.data(); h.sZ = d->msZ.data(); h.errp = d->merrp.data();
+    const Code& c = *d->code;
+    h.code = &c;
     h.chkVar = syndrome_table(d);
     h.varEdge = variable_table(d);
+    // the depolarising front end hands the wave-circulant engine its syndromes as bit rows and its
+    // packed errors at word-aligned rows (72 + 156 instead of 549 + 154 B per P61 sample)
+    const bool bits = src == MC_SRC_PHILOX && d->engine != QEC_ENGINE_SPARSE;
+    if (bits) {
+        h.sXp = reinterpret_cast<uint32_t*>(d->msX.data());
+        h.sZp = reinterpret_cast<uint32_t*>(d->msZ.data());
+        h.errp_words = true;
+    } else {
+        h.sX = d->msX.data(); h.sZ = d->msZ.data();
+    }
+    h.errp = d->merrp.data();
     int rc = launch_mc_errors_syndrome(src, h, st);
     if (rc) return rc;
     if (ev0) QEC_HIP_CHECK(hipEventRecord(ev0, st));
     rc = dispatch_decode(d, d->msX.data(), d->msZ.data(), h.B, p, maxIter, stop, nullptr, nullptr, nullptr,
-                         d->mrec.data(), want_iters ? d->mit.data() : nullptr, nullptr, st);
+                         d->mrec.data(), want_iters ? d->mit.data() : nullptr, nullptr, st, bits);
     if (rc) return rc;
     if (ev1) QEC_HIP_CHECK(hipEventRecord(ev1, st));
-    return launch_statistics_packed(*d->code, d->imp_cols.data(), d->merrp.data(), d->mrec.data(),
-                                    want_iters ? d->mit.data() : nullptr, h.B, d->mcount.data(), st);
+    const int nb = (c.n + 7) / 8;
+    return launch_statistics_packed(c, d->imp_cols.data(), d->merrp.data(), bits ? 4 * ((2 * nb + 3) / 4) : 2 * nb,
+                                    d->mrec.data(), want_iters ? d->mit.data() : nullptr, h.B, d->mcount.data(), st);
 }
 
 int mc_fetch_counters(qec_decoder* d, unsigned long long* out)
@@ -1054,7 +1072,7 @@ int qec_statistics_packed_dev(qec_decoder* d, const uint8_t* errp, const uint8_t
     int rc = single_device_only(d, "qec_statistics_packed_dev");
     if (rc) return rc;
     QEC_DEVICE_SCOPE(d->device);
-    return launch_statistics_packed(*d->code, d->imp_cols.data(), errp, records, iters, (long long)B,
+    return launch_statistics_packed(*d->code, d->imp_cols.data(), errp, 2 * ((d->code->n + 7) / 8), records, iters, (long long)B,
                                     reinterpret_cast<unsigned long long*>(counters), static_cast<hipStream_t>(stream));
 }
 

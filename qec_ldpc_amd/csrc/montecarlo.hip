@@ -186,7 +186,7 @@ __device__ __forceinline__ bool logical_from_columns(const unsigned long long* r
 // workgroup serialise at L2: 16 384 four-wave workgroups x 8 counters cost ~190 us per 65 536
 // samples, profiles/r02/mc_r02f_trace.csv).
 constexpr int kStatBlockWaves = 16;
-constexpr int kStatMaxBlocks = 512;
+constexpr int kStatMaxBlocks = 256;
 
 __device__ __forceinline__ void stat_flush(unsigned long long (*part)[C_N + 2], const unsigned long long* c, int nc,
                                            unsigned long long* __restrict__ counters)
@@ -426,13 +426,16 @@ __global__ __launch_bounds__(64 * kMcWaves) void mc_errors_syndrome_kernel(const
 
 // ---- fused front end for the depolarising sampler (the gap walk) ---------------------
 // One lane per sample: the lane walks its sample (gap_walk) and, for every hit, sets the qubit's
-// bits in the sample's packed-error words and flips the qubit's checks in its syndrome bit set
-// (both in LDS, this lane's own region: w32 = ew + sw words, errors in the decision-record layout,
-// then mX + mZ syndrome bits).  Then the wave writes its samples' contiguous output blocks (sX, sZ,
-// errp) as coalesced dwords (write_block).  QEC_GAP_WRITE = 0 has each lane write its own sample's
-// rows instead (write_row): 4x fewer instructions, but every store scatters over 64 rows, which
-// measured slower (P61, 65 536 samples at p = 0.002: 62 vs 41 us).  Nothing but syndromes and packed
-// errors reaches HBM, and the sampler costs words per hit, not per qubit.
+// bits in the sample's packed-error words and flips the qubit's checks in its syndrome bit sets
+// (both in LDS, this lane's own region of w32 = ew + wX + wZ words: errors in the decision-record
+// layout, then the X checks' bits, then the Z checks').  Then the wave writes its samples'
+// contiguous output blocks as coalesced dwords (write_block): syndromes as bytes (sX, sZ, the
+// public layout) or as bit rows (sXp [B][wX], sZp [B][wZ] words, the Monte-Carlo pipeline's
+// layout: 72 instead of 549 B per P61 sample), packed errors at a row stride of 2 nb bytes (the
+// public layout) or 4 ew (word-aligned rows, a word copy).  Each lane writing its own sample's
+// rows instead (4x fewer instructions, but every store scattered over 64 rows) measured slower:
+// 62 vs 41 us per 65 536 P61 samples at p = 0.002.  Nothing but syndromes and packed errors
+// reaches HBM, and the sampler costs words per hit, not per qubit.
 constexpr int kGapWaves = 4;
 
 struct GapArgs {
@@ -441,15 +444,17 @@ struct GapArgs {
     long long B;
     int n, nb, mX, mZ, P, L, J, K;
     int spw;           // samples per wave
-    int ew, w32;       // LDS words per sample: packed errors, then syndrome bits
-    uint32_t magicX, magicZ, magicE;  // ceil(2^32 / d) for d = mX, mZ, 2 nb
-    uint8_t* sX;
+    int ew, wX, wZ, w32;  // LDS words per sample: packed errors, X bits, Z bits; total
+    int estride;       // errp row stride in bytes: 2 nb or 4 ew
+    uint32_t magicX, magicZ, magicE, magicWX, magicWZ, magicEW;  // ceil(2^32 / d)
+    uint8_t* sX;       // byte rows (nullable when sXp is given)
     uint8_t* sZ;
+    uint32_t* sXp;     // bit rows (nullable)
+    uint32_t* sZp;
     uint8_t* errp;     // nullable
     const int32_t* varEdge;  // non-QC codes: n x dvX then n x dvZ edge ids; check = edge / dc
     int dc, dvX, dvZ;
     int ablate;              // timing experiments only (QEC_GAP_ABLATE; wrong outputs): 1 no write-out, 2 no walk
-    int block_write;         // QEC_GAP_WRITE = 1: wave-block write-out (write_block)
     int EX[128], EZ[128];    // QC codes
 };
 
@@ -471,32 +476,12 @@ __device__ __forceinline__ void write_block(uint8_t* __restrict__ dst, int tot, 
     if (tail < tot) dst[tail] = (uint8_t)f(tail);
 }
 
-// One lane's output row of len bytes at dst (any alignment): head bytes up to 4-byte alignment,
-// dwords, tail bytes; byte(c) = byte c, dword(c) = bytes c .. c+3 (little-endian).
-template <class Byte, class Dword>
-__device__ __forceinline__ void write_row(uint8_t* __restrict__ dst, int len, Byte&& byte, Dword&& dword)
+// Words [0, tot) of a wave's word-aligned output block, word k = f(k).
+template <class F>
+__device__ __forceinline__ void write_words(uint32_t* __restrict__ dst, int tot, int lane, F&& f)
 {
-    const int h = min((int)((0u - (uint32_t)(uintptr_t)dst) & 3u), len);
-    for (int c = 0; c < h; ++c) dst[c] = (uint8_t)byte(c);
-    const int nd = (len - h) >> 2;
-    uint32_t* __restrict__ d32 = reinterpret_cast<uint32_t*>(dst + h);
-    for (int t = 0; t < nd; ++t) d32[t] = dword(h + 4 * t);
-    for (int c = h + 4 * nd; c < len; ++c) dst[c] = (uint8_t)byte(c);
-}
-
-// bits c .. c+3 of a bit set (words w) as four 0/1 bytes
-__device__ __forceinline__ uint32_t bits4_to_bytes(const uint32_t* __restrict__ w, int c)
-{
-    const uint64_t pair = (uint64_t)w[c >> 5] | ((c & 31) > 28 ? (uint64_t)w[(c >> 5) + 1] << 32 : 0ull);
-    const uint32_t nib = (uint32_t)(pair >> (c & 31)) & 0xFu;
-    return (nib * 0x204081u) & 0x01010101u;  // nibble bit k -> byte k (the four shifted copies never overlap)
-}
-// bytes c .. c+3 of a byte string held in words w
-__device__ __forceinline__ uint32_t bytes4(const uint32_t* __restrict__ w, int c)
-{
-    const int sh = 8 * (c & 3);
-    const uint32_t lo = w[c >> 2];
-    return sh == 0 ? lo : (lo >> sh) | (w[(c >> 2) + 1] << (32 - sh));
+#pragma unroll 4
+    for (int t = lane; t < tot; t += 64) dst[t] = f(t);
 }
 
 __global__ __launch_bounds__(64 * kGapWaves) void mc_gap_kernel(const GapArgs a)
@@ -515,9 +500,11 @@ __global__ __launch_bounds__(64 * kGapWaves) void mc_gap_kernel(const GapArgs a)
     const long long b0 = ((long long)blockIdx.x * kGapWaves + wv) * a.spw;
     if (b0 >= a.B) return;  // wave-local from here on
     const int ns = (int)(a.B - b0 < a.spw ? a.B - b0 : a.spw);
+    const int w32 = a.w32, ew = a.ew, wX = a.wX, wZ = a.wZ;
     if (lane < ns && a.gp.thr != 0 && a.ablate != 2) {
-        uint32_t* __restrict__ mine = reg + lane * a.w32;
-        uint32_t* __restrict__ syn = mine + a.ew;
+        uint32_t* __restrict__ mine = reg + lane * w32;
+        uint32_t* __restrict__ synX = mine + ew;
+        uint32_t* __restrict__ synZ = synX + wX;
         const int zb = 8 * a.nb, P = a.P, L = a.L;
         gap_walk(a.gp, a.start + (uint64_t)(b0 + lane), n, T, [&](int v, uint32_t t) {
             const bool ex = t != 2, ez = t != 0;
@@ -530,62 +517,63 @@ __global__ __launch_bounds__(64 * kGapWaves) void mc_gap_kernel(const GapArgs a)
                     for (int r = 0; r < a.J; ++r) {
                         const int d = j - E[r * L + l];
                         const int c = r * P + (d < 0 ? d + P : d);
-                        atomicXor(&syn[c >> 5], 1u << (c & 31));
+                        atomicXor(&synX[c >> 5], 1u << (c & 31));
                     }
                 if (ez)
                     for (int r = 0; r < a.K; ++r) {
                         const int d = j - E[(a.J + r) * L + l];
-                        const int c = a.mX + r * P + (d < 0 ? d + P : d);
-                        atomicXor(&syn[c >> 5], 1u << (c & 31));
+                        const int c = r * P + (d < 0 ? d + P : d);
+                        atomicXor(&synZ[c >> 5], 1u << (c & 31));
                     }
             } else {
                 if (ex)
                     for (int k = 0; k < a.dvX; ++k) {
                         const int c = a.varEdge[(size_t)v * a.dvX + k] / a.dc;
-                        atomicXor(&syn[c >> 5], 1u << (c & 31));
+                        atomicXor(&synX[c >> 5], 1u << (c & 31));
                     }
                 if (ez)
                     for (int k = 0; k < a.dvZ; ++k) {
-                        const int c = a.varEdge[(size_t)n * a.dvX + (size_t)v * a.dvZ + k] / a.dc;  // Z ids are offset by mX dc
-                        atomicXor(&syn[c >> 5], 1u << (c & 31));
+                        // Z edge ids are offset by mX dc: check mX + c
+                        const int c = a.varEdge[(size_t)n * a.dvX + (size_t)v * a.dvZ + k] / a.dc - a.mX;
+                        atomicXor(&synZ[c >> 5], 1u << (c & 31));
                     }
             }
         });
     }
     wave_sync();
     if (a.ablate == 1) return;
-    const int w32 = a.w32, ew = a.ew;
-    if (!a.block_write) {
-        if (lane < ns) {
-            const long long b = b0 + lane;
-            const uint32_t* __restrict__ mine = reg + lane * w32;
-            const uint32_t* __restrict__ syn = mine + ew;
-            write_row(a.sX + b * a.mX, a.mX, [&](int c) { return (syn[c >> 5] >> (c & 31)) & 1u; },
-                      [&](int c) { return bits4_to_bytes(syn, c); });
-            write_row(a.sZ + b * a.mZ, a.mZ, [&](int c) { return (syn[(a.mX + c) >> 5] >> ((a.mX + c) & 31)) & 1u; },
-                      [&](int c) { return bits4_to_bytes(syn, a.mX + c); });
-            if (a.errp != nullptr) {
-                const int eb = 2 * a.nb;
-                write_row(a.errp + b * eb, eb, [&](int c) { return (mine[c >> 2] >> (8 * (c & 3))) & 0xFFu; },
-                          [&](int c) { return bytes4(mine, c); });
-            }
-        }
-        return;
-    }
-    write_block(a.sX + b0 * a.mX, ns * a.mX, lane, [&](int k) -> uint32_t {
-        const int s = qdiv(k, a.magicX), c = k - s * a.mX;
-        return (reg[s * w32 + ew + (c >> 5)] >> (c & 31)) & 1u;
-    });
-    write_block(a.sZ + b0 * a.mZ, ns * a.mZ, lane, [&](int k) -> uint32_t {
-        const int s = qdiv(k, a.magicZ), c = a.mX + (k - s * a.mZ);
-        return (reg[s * w32 + ew + (c >> 5)] >> (c & 31)) & 1u;
-    });
-    if (a.errp != nullptr) {
-        const int eb = 2 * a.nb;
-        write_block(a.errp + b0 * eb, ns * eb, lane, [&](int k) -> uint32_t {
-            const int s = qdiv(k, a.magicE), c = k - s * eb;
-            return (reg[s * w32 + (c >> 2)] >> (8 * (c & 3))) & 0xFFu;
+    if (a.sXp != nullptr) {
+        write_words(a.sXp + b0 * wX, ns * wX, lane, [&](int k) {
+            const int s = qdiv(k, a.magicWX);
+            return reg[s * w32 + ew + (k - s * wX)];
         });
+        write_words(a.sZp + b0 * wZ, ns * wZ, lane, [&](int k) {
+            const int s = qdiv(k, a.magicWZ);
+            return reg[s * w32 + ew + wX + (k - s * wZ)];
+        });
+    } else {
+        write_block(a.sX + b0 * a.mX, ns * a.mX, lane, [&](int k) -> uint32_t {
+            const int s = qdiv(k, a.magicX), c = k - s * a.mX;
+            return (reg[s * w32 + ew + (c >> 5)] >> (c & 31)) & 1u;
+        });
+        write_block(a.sZ + b0 * a.mZ, ns * a.mZ, lane, [&](int k) -> uint32_t {
+            const int s = qdiv(k, a.magicZ), c = k - s * a.mZ;
+            return (reg[s * w32 + ew + wX + (c >> 5)] >> (c & 31)) & 1u;
+        });
+    }
+    if (a.errp != nullptr) {
+        if (a.estride == 4 * ew) {
+            write_words(reinterpret_cast<uint32_t*>(a.errp) + b0 * ew, ns * ew, lane, [&](int k) {
+                const int s = qdiv(k, a.magicEW);
+                return reg[s * w32 + (k - s * ew)];
+            });
+        } else {
+            const int eb = 2 * a.nb;
+            write_block(a.errp + b0 * eb, ns * eb, lane, [&](int k) -> uint32_t {
+                const int s = qdiv(k, a.magicE), c = k - s * eb;
+                return (reg[s * w32 + (c >> 2)] >> (8 * (c & 3))) & 0xFFu;
+            });
+        }
     }
 }
 
@@ -599,11 +587,14 @@ __global__ __launch_bounds__(64 * kGapWaves) void mc_gap_kernel(const GapArgs a)
 // needs the I-P columns (no syndrome failure, nonzero residual).  NJ = 0: any code, one sample at
 // a time.
 constexpr int kMaxRecWords = 80;  // 2 nb <= 640 bytes
+#ifndef QEC_STAT_U
+#define QEC_STAT_U 4
+#endif
 
 template <int NJ, int U>
 __global__ __launch_bounds__(64 * kStatBlockWaves) void statistics_packed_kernel(
-    const uint8_t* __restrict__ errp, const uint8_t* __restrict__ rec, const int32_t* __restrict__ iters, long long B,
-    int n, int nb, const uint64_t* __restrict__ imp_cols, int imp_cw, unsigned long long* __restrict__ counters)
+    const uint8_t* __restrict__ errp, int estride, const uint8_t* __restrict__ rec, const int32_t* __restrict__ iters,
+    long long B, int n, int nb, const uint64_t* __restrict__ imp_cols, int imp_cw, unsigned long long* __restrict__ counters)
 {
     __shared__ unsigned long long part[kStatBlockWaves][C_N + 2];
     __shared__ __attribute__((aligned(8))) uint8_t sres[kStatBlockWaves][8 * kMaxRecWords];
@@ -616,23 +607,22 @@ __global__ __launch_bounds__(64 * kStatBlockWaves) void statistics_packed_kernel
     for (long long b0 = ((long long)blockIdx.x * kStatBlockWaves + wv) * U; b0 < B; b0 += step) {
         uint32_t any[U];  // per lane and sample: bit 0 x errors, bit 1 z errors, bit 2 residual
         uint8_t f[U];
+        // branch-free loads (indices clamped into the batch and the row, results masked after): loads
+        // under a condition are each followed by their own wait
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const long long b = b0 + u;
+            const long long b = b0 + u < B ? b0 + u : B - 1;
+            f[u] = rec[b * recB + 2 * nb];
             any[u] = 0;
-            f[u] = 0;
-            if (b < B) {
-                f[u] = rec[b * recB + 2 * nb];
 #pragma unroll
-                for (int j = 0; j < (NJ > 0 ? NJ : 1); ++j) {
-                    for (int jj = j; jj < (NJ > 0 ? j + 1 : nj); ++jj) {
-                        const int t = lane + 64 * jj;
-                        if (t < 2 * nb) {
-                            const uint8_t e = errp[b * 2 * nb + t];
-                            const uint8_t r = e ^ rec[b * recB + t];
-                            any[u] |= (e != 0 ? (t < nb ? 1u : 2u) : 0u) | (r != 0 ? 4u : 0u);
-                        }
-                    }
+            for (int j = 0; j < (NJ > 0 ? NJ : 1); ++j) {
+                for (int jj = j; jj < (NJ > 0 ? j + 1 : nj); ++jj) {
+                    const int t = lane + 64 * jj;
+                    const int tc = t < 2 * nb ? t : 0;
+                    const uint8_t e = errp[b * estride + tc];
+                    const uint8_t r = e ^ rec[b * recB + tc];
+                    const uint32_t m = (e != 0 ? (t < nb ? 1u : 2u) : 0u) | (r != 0 ? 4u : 0u);
+                    any[u] |= t < 2 * nb ? m : 0u;
                 }
             }
         }
@@ -646,7 +636,7 @@ __global__ __launch_bounds__(64 * kStatBlockWaves) void statistics_packed_kernel
             // error itself, the common case) has (I-P) r = 0 without reading a column
             if (!(dEX || dEZ) && imp_cw > 0 && __any(any[u] & 4u)) {
                 for (int t = lane; t < 8 * nw; t += 64)
-                    sres[wv][t] = t < 2 * nb ? (uint8_t)(errp[b * 2 * nb + t] ^ rec[b * recB + t]) : (uint8_t)0;
+                    sres[wv][t] = t < 2 * nb ? (uint8_t)(errp[b * estride + t] ^ rec[b * recB + t]) : (uint8_t)0;
                 wave_sync();
                 logical = logical_from_columns<true>(reinterpret_cast<const unsigned long long*>(sres[wv]), nw, n, nb,
                                                      imp_cols, imp_cw, lane);
@@ -709,14 +699,12 @@ static int launch_mc_gap(const McArgsHost& h, hipStream_t st)
     a.start = h.start;
     a.B = h.B;
     a.n = c.n; a.nb = (c.n + 7) / 8; a.mX = c.mX; a.mZ = c.mZ; a.P = c.P; a.L = c.L; a.J = c.J; a.K = c.K;
-    a.sX = h.sX; a.sZ = h.sZ; a.errp = h.errp;
+    a.sX = h.sX; a.sZ = h.sZ; a.sXp = h.sXp; a.sZp = h.sZp; a.errp = h.errp;
     a.varEdge = h.varEdge;
     a.dc = c.L; a.dvX = c.J; a.dvZ = c.K;
     {
         static const int ab = [] { const char* e = std::getenv("QEC_GAP_ABLATE"); return e ? std::atoi(e) : 0; }();
         a.ablate = ab;
-        static const int bw = [] { const char* e = std::getenv("QEC_GAP_WRITE"); return e ? std::atoi(e) : 1; }();
-        a.block_write = bw;
     }
     if (a.varEdge == nullptr) {
         if (!c.is_qc || c.J * c.L > 128 || c.K * c.L > 128)
@@ -725,12 +713,16 @@ static int launch_mc_gap(const McArgsHost& h, hipStream_t st)
         for (size_t k = 0; k < c.EZ.size(); ++k) a.EZ[k] = c.EZ[k];
     }
     a.ew = (2 * a.nb + 3) / 4;
-    a.w32 = a.ew + (c.mX + c.mZ + 31) / 32;
+    a.wX = (c.mX + 31) / 32;
+    a.wZ = (c.mZ + 31) / 32;
+    a.w32 = a.ew + a.wX + a.wZ;
+    a.estride = h.errp_words ? 4 * a.ew : 2 * a.nb;
     // at most 16 KiB of sample state per wave
     a.spw = std::max(1, std::min(gap_spw_default(), 16384 / (4 * a.w32)));
     if ((long long)a.spw * std::max<long long>({(long long)c.mX, (long long)c.mZ, 2LL * a.nb}) >= 65536)
         return fail(QEC_ERR_UNSUPPORTED, "mc front end: code too long");
     a.magicX = magic_of(c.mX); a.magicZ = magic_of(c.mZ); a.magicE = magic_of(2 * a.nb);
+    a.magicWX = magic_of(a.wX); a.magicWZ = magic_of(a.wZ); a.magicEW = magic_of(a.ew);
     const int ne = a.varEdge ? 0 : (c.J + c.K) * c.L;
     const size_t smem = 4 * ((size_t)c.n + 1 + ne + (size_t)kGapWaves * a.spw * a.w32);
     if (smem > 64 * 1024) return fail(QEC_ERR_UNSUPPORTED, "mc front end: code too long for the LDS stage");
@@ -783,7 +775,7 @@ int launch_mc_errors_syndrome(int src, const McArgsHost& h, hipStream_t st)
     return launch_check("mc_errors_syndrome");
 }
 
-int launch_statistics_packed(const Code& c, const uint64_t* imp_cols, const uint8_t* errp, const uint8_t* rec,
+int launch_statistics_packed(const Code& c, const uint64_t* imp_cols, const uint8_t* errp, int estride, const uint8_t* rec,
                              const int32_t* iters, long long B, unsigned long long* counters, hipStream_t st)
 {
     if (B <= 0) return QEC_OK;
@@ -791,11 +783,12 @@ int launch_statistics_packed(const Code& c, const uint64_t* imp_cols, const uint
     if ((2 * nb + 7) / 8 > kMaxRecWords || c.imp_col_words > 64)
         return fail(QEC_ERR_UNSUPPORTED, "packed statistics kernel: code too long");
     const int nj = (8 * ((2 * nb + 7) / 8) + 63) / 64;
-    constexpr int U = 4;
-    const long long blocks = std::min<long long>((B + kStatBlockWaves * U - 1) / (kStatBlockWaves * U), kStatMaxBlocks);
+    constexpr int U = QEC_STAT_U;
+    static const int maxb = [] { const char* e = std::getenv("QEC_STAT_BLOCKS"); const int v = e ? std::atoi(e) : 0; return v > 0 ? v : kStatMaxBlocks; }();
+    const long long blocks = std::min<long long>((B + kStatBlockWaves * U - 1) / (kStatBlockWaves * U), maxb);
     auto kern = nj == 1 ? statistics_packed_kernel<1, U> : nj == 3 ? statistics_packed_kernel<3, U> : statistics_packed_kernel<0, 1>;
-    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(64 * kStatBlockWaves), 0, st, errp, rec, iters, B, c.n, nb,
-                       imp_cols, c.imp_col_words, counters);
+    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(64 * kStatBlockWaves), 0, st, errp, estride, rec, iters, B,
+                       c.n, nb, imp_cols, c.imp_col_words, counters);
     return launch_check("statistics_packed");
 }
 

@@ -72,7 +72,10 @@ struct McArgsHost {
     const uint8_t* z = nullptr;
     uint8_t* sX = nullptr;
     uint8_t* sZ = nullptr;
+    uint32_t* sXp = nullptr;        // PHILOX only: syndromes as bit rows [B][ceil(mX/32)] words instead
+    uint32_t* sZp = nullptr;
     uint8_t* errp = nullptr;        // [B][2 ceil(n/8)], nullable
+    bool errp_words = false;        // PHILOX only: errp rows padded to whole words (4 ceil(2 ceil(n/8) / 4) B)
     const int32_t* chkVar = nullptr;  // non-QC codes: check -> variables (BYTES, DRAWS)
     const int32_t* varEdge = nullptr; // non-QC codes: variable -> edges (PHILOX, the gap walk)
     long long B = 0;

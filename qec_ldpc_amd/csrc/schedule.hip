@@ -112,6 +112,34 @@ __global__ __launch_bounds__(kHistThreads) void schedule_hist_kernel(const uint8
     if (t < kBuckets) counts[(long long)blockIdx.x * kBuckets + t] = h[t];
 }
 
+// The same weights from bit rows (sX [B][wX], sZ [B][wZ] words; the Monte-Carlo pipeline's
+// layout): one thread per syndrome, popcounts of its words.
+__global__ __launch_bounds__(kHistThreads) void schedule_hist_bits_kernel(const uint32_t* __restrict__ sX,
+                                                                        const uint32_t* __restrict__ sZ, long long B,
+                                                                        int wX, int wZ, int chunk,
+                                                                        uint8_t* __restrict__ key,
+                                                                        uint32_t* __restrict__ counts,
+                                                                        uint32_t* __restrict__ zero_merge)
+{
+    __shared__ uint32_t h[kBuckets];
+    const int t = threadIdx.x;
+    const long long r0 = (long long)blockIdx.x * chunk;
+    const long long r1 = r0 + chunk < B ? r0 + chunk : B;
+    if (t < kBuckets) h[t] = 0;
+    __syncthreads();
+    for (long long b = r0 + t; b < r1; b += kHistThreads) {
+        uint32_t w = 0;
+        for (int k = 0; k < wX; ++k) w += __popc(sX[b * wX + k]);
+        for (int k = 0; k < wZ; ++k) w += __popc(sZ[b * wZ + k]);
+        const int bk = kBuckets - 1 - (int)(w < kBuckets - 1 ? w : kBuckets - 1);
+        key[b] = (uint8_t)bk;
+        atomicAdd(&h[bk], 1u);
+        if (zero_merge) zero_merge[b] = 0u;
+    }
+    __syncthreads();
+    if (t < kBuckets) counts[(long long)blockIdx.x * kBuckets + t] = h[t];
+}
+
 // Bucket offsets: workgroup k scans column k of the [chunks][256] count matrix (one thread per
 // chunk, LDS scan), writes each chunk's exclusive prefix in place and the bucket total.  About
 // 2 KiB of the matrix per workgroup; the previous design, every scatter workgroup re-reading
@@ -186,11 +214,11 @@ size_t schedule_workspace_bytes(long long B, int, int)
 // Fills the workspace (schedule_workspace_bytes bytes) and returns in *perm_out the
 // heaviest-first order of the batch.  zero_merge (nullable): B words the hist pass zeroes on
 // the way (the sector-split decode merges its two sectors' flags there, bp_decode.hip).
-int launch_schedule(const uint8_t* sX, const uint8_t* sZ, long long B, int mX, int mZ, void* ws,
+int launch_schedule(const uint8_t* sX, const uint8_t* sZ, bool sbits, long long B, int mX, int mZ, void* ws,
                     uint32_t* zero_merge, int32_t** perm_out, hipStream_t st)
 {
     if (B > schedule_max_batch()) return fail(QEC_ERR_ARG, "schedule: batch too large to order");
-    const bool shortrows = mX + mZ <= kShortRows;
+    const bool shortrows = sbits || mX + mZ <= kShortRows;
     int nch = 0;
     const int chunk = chunk_of(B, shortrows ? kHistThreads : 256, &nch);
     uint8_t* p = static_cast<uint8_t*>(ws);
@@ -199,7 +227,11 @@ int launch_schedule(const uint8_t* sX, const uint8_t* sZ, long long B, int mX, i
     uint32_t* totals = counts + (size_t)kMaxChunks * kBuckets;
     uint8_t* key = reinterpret_cast<uint8_t*>(totals + kBuckets);
     *perm_out = perm;
-    if (shortrows)
+    if (sbits)
+        hipLaunchKernelGGL(schedule_hist_bits_kernel, dim3(nch), dim3(kHistThreads), 0, st,
+                           reinterpret_cast<const uint32_t*>(sX), reinterpret_cast<const uint32_t*>(sZ), B, (mX + 31) / 32,
+                           (mZ + 31) / 32, chunk, key, counts, zero_merge);
+    else if (shortrows)
         hipLaunchKernelGGL(schedule_hist_kernel<1>, dim3(nch), dim3(kHistThreads), 0, st, sX, sZ, B, mX, mZ, chunk, key,
                            counts, zero_merge);
     else

@@ -106,6 +106,10 @@ namespace qec {
 #ifndef QEC_ZERO_SYNDROME
 #define QEC_ZERO_SYNDROME 1
 #endif
+//   QEC_SYN_EARLY    syndrome stop: iteration 0 tests the syndrome before forming its messages
+#ifndef QEC_SYN_EARLY
+#define QEC_SYN_EARLY 1
+#endif
 //   QEC_TRACK_FROM   first iteration whose var pass tests whether the sector became hard
 #ifndef QEC_TRACK_FROM
 #define QEC_TRACK_FROM 2
@@ -959,13 +963,73 @@ __device__ __forceinline__ float table0_entry(float pp, int e)
     return P1 / (P0 + P1);
 }
 
+// Bit idx of hdpat: a variable whose R checks have syndrome pattern idx decides 1 after iteration 0
+// (some table entry >= 0.5); of cvpat: its R messages all lie outside (0.01, 0.99).  Called with every
+// lane of the wave active (the ballots must see lanes 0 .. 2^R - 1).
+template <int R>
+__device__ __forceinline__ void pattern_masks(const float* __restrict__ tab, unsigned long long& hdpat,
+                                              unsigned long long& cvpat)
+{
+    const int li = (int)__lane_id();
+    bool hp = false, cp = true;
+    if (li < (1 << R)) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const float t = tab[li * R + r];
+            hp |= t >= 0.5f;
+            cp &= outside(t);
+        }
+    }
+    hdpat = __ballot(li < (1 << R) && hp);
+    cvpat = __ballot(li < (1 << R) && cp);
+}
+
 template <int R, int L, int SEC, int STOP, class SH>
 __device__ __forceinline__ bool iteration0(const BpArgs& a, float (&msg)[R][L], uint32_t sbits, const Lane& ln,
-                                           const float* __restrict__ tab, uint32_t& hd_out)
+                                           const float* __restrict__ tab, uint32_t& hd_out, bool& cv_out,
+                                           bool& msg_out, unsigned long long hdpat, unsigned long long cvpat)
 {
     const int P = SH::P(a);
     const int* et = SH::template table<SEC>(a);
     constexpr bool HD = STOP == QEC_STOP_SYNDROME;
+    msg_out = true;
+    if constexpr (HD && QEC_SYN_EARLY && L * R <= 64) {
+        // Syndrome stop: a variable's hard decision after this iteration, and whether its R
+        // messages lie outside (0.01, 0.99), depend only on its syndrome pattern idx, so they come
+        // from two 2^R-bit masks before any message is formed; the messages themselves (table
+        // reads and return rotations) are only built when some group goes on -- a group that
+        // stops here needs just those two bits for its outputs (decode_sector; hdpat / cvpat from
+        // pattern_masks).
+        uint64_t idxs = 0;
+        uint32_t hdmask = 0;
+        bool cv = true;
+#pragma unroll
+        for (int l = 0; l < L; ++l) {
+            int idx = 0;
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+                idx |= ((rot_i<SH>((int)sbits, ln, SH::template shift<SEC, L>(et, r, l)) >> r) & 1) << r;
+            idxs |= (uint64_t)idx << (R * l);
+            hdmask |= (uint32_t)((hdpat >> idx) & 1ull) << l;
+            cv &= ((cvpat >> idx) & 1ull) != 0ull;
+        }
+        const bool stop = group_all_sh<SH>(lane_syndrome_ok<R, L, SEC, SH>(a, hdmask, sbits, ln), ln, P);
+        hd_out = hdmask;
+        cv_out = cv;
+        msg_out = a.q != nullptr || __any(ln.live && !stop);  // q_final reads the messages
+        if (msg_out) {
+#pragma unroll
+            for (int l = 0; l < L; ++l) {
+                const int idx = (int)((idxs >> (R * l)) & ((1u << R) - 1u));
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const int sh = SH::template shift<SEC, L>(et, r, l);
+                    msg[r][l] = rot<SH>(tab[idx * R + r], ln, sh == 0 ? 0 : P - sh);
+                }
+            }
+        }
+        return stop;
+    }
     uint32_t hdmask = 0;
 #pragma unroll
     for (int l = 0; l < L; ++l) {
@@ -1152,9 +1216,14 @@ __device__ __forceinline__ void decode_sector(const BpArgs& a, Lane& ln, uint32_
     // syndrome test the same test, so they are reused (group-uniform).
     uint32_t hd_last = 0;
     bool syn_last = false, hd_valid = false;
+    // iteration 0 of the syndrome stop may leave the messages unformed (every group stopped there):
+    // then cv0 is each lane's convergence test of them (iteration0)
+    bool cv0 = true, msg_built = true;
+    unsigned long long hdpat = 0, cvpat = 0;
+    if constexpr (STOP == QEC_STOP_SYNDROME && QEC_SYN_EARLY && QEC_TABLE0) pattern_masks<R>(tab0, hdpat, cvpat);
     if (QEC_TABLE0 && N >= 2 && active) {  // iteration 0 by table (see iteration0)
         ++it;
-        syn_last = iteration0<R, L, SEC, STOP, SH>(a, msg, sbits, ln, tab0, hd_last);
+        syn_last = iteration0<R, L, SEC, STOP, SH>(a, msg, sbits, ln, tab0, hd_last, cv0, msg_built, hdpat, cvpat);
         hd_valid = true;
         if (syn_last) active = false;
         if constexpr (QEC_PHASE_STATS) ph_soft += 1;
@@ -1212,7 +1281,7 @@ __device__ __forceinline__ void decode_sector(const BpArgs& a, Lane& ln, uint32_
     uint32_t hdmask = 0;  // e[v] of this lane's variables (l, (i + C[l]) mod P), bit l
     if (STOP == QEC_STOP_SYNDROME && all_live(hd_valid, in_range)) {
         // the last iteration's hard decision and syndrome test are the post-processing's
-        conv = group_all_sh<SH>(lane_converged<R, L>(msg), ln, P);
+        conv = group_all_sh<SH>(__any(in_range && msg_built) ? lane_converged<R, L>(msg) : cv0, ln, P);
         hdmask = hd_last;
         syn_ok = syn_last;
     } else if (TU::kSaturate && all_live(st_agreed, in_range)) {

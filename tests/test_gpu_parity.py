@@ -89,7 +89,24 @@ def test_ragged_batches(env, B):
     """Batch sizes that leave partial wavefront groups (P7 packs 9 syndromes per wave)."""
     for key in ("P7", "P61"):
         sX, sZ = mixed_inputs(env[key][0], max(B, 4), 11, 0.02)
-        check(env, key, sX[:B], sZ[:B], 0.02, 15, "ref", want_q=False)
+        for stop in ("ref", "fixed", "syndrome"):
+            check(env, key, sX[:B], sZ[:B], 0.02, 15, stop, want_q=False)
+
+
+@pytest.mark.parametrize("key", ["P7", "P61"])
+@pytest.mark.parametrize("p", [0.001, 0.002, 0.01, 0.05])
+def test_syndrome_stop_without_messages(env, key, p):
+    """The syndrome stop's shortcuts that apply only when no final messages are requested: a
+    sector with a zero syndrome skips to its known outputs, and iteration 0 tests the syndrome
+    before forming its messages (bp_decode.hip).  Low p (most sectors zero or stopping at
+    iteration 0), a ragged batch whose last P7 wave holds one syndrome, against the oracle."""
+    code = env[key][0]
+    x, z = depolarizing_errors(code.n, 31337, 1000, p)
+    sX, sZ = code.syndrome(0, x), code.syndrome(1, z)
+    sX[:50] = 0
+    sZ[25:75] = 0
+    check(env, key, sX, sZ, p, 30, "syndrome", want_q=False)
+    check(env, key, sX[:10], sZ[:10], p, 30, "syndrome", want_q=False)
 
 
 def test_empty_batch(env):

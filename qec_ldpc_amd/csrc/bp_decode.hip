@@ -1433,7 +1433,7 @@ using KernelFn = void (*)(const BpArgs);
 using TuneP61 = Tune<5, true, false, true, true, false, true, 1, 2, 4>;
 struct TuneP61MinReg : TuneP61 {};
 using ShiftsP61 = GeneratedShifts<4, 5, 10, 61, 9, 49, TuneP61::kRelabel, TuneP61::kMaskSelect>;
-using TuneP7 = Tune<8, false, false, true, true, true, false, 0, 4, 6>;
+using TuneP7 = Tune<8, true, false, true, true, true, false, 1, 4, 7>;
 struct TuneP7MinReg : TuneP7 {};
 using ShiftsP7 = GeneratedShifts<3, 3, 6, 7, 2, 3, TuneP7::kRelabel, TuneP7::kMaskSelect>;
 #ifndef QEC_P61_MINREG
@@ -1536,8 +1536,8 @@ static Variant gen()
 // 1.75 vs 2.16 ms at p = 0.05; its syndrome-stop kernels spill badly at 5 waves (450 scratch
 // loads, 1.01 vs 0.50 ms) and keep 4 (profiles/r01/session7/cmp_s7l-n_*.txt).  Round 2: without
 // the agreement test (kAgree) the syndrome-stop kernels are spill-free, P61 at 4 waves (125 VGPRs)
-// and P7 at 6 (75 VGPRs; as fast as 7 waves with 9 spills and 1-4 % faster than 8 with 40-70,
-// profiles/r02/syn_variants_r02s3i.txt).
+// and P7 at 7 (with the lane relabelling and gather pipelining P7 now takes too, 2-5 % faster
+// at every stop rule: 260 instead of 456 static ds_bpermute; profiles/r02/p7_variants_r02s3{s,t}.txt).
 static Variant gen_p61()
 {
     Variant v = gen<4, 5, 10, 61, 9, 49, TuneP61>();

@@ -110,6 +110,11 @@ namespace qec {
 #ifndef QEC_SYN_EARLY
 #define QEC_SYN_EARLY 1
 #endif
+//   QEC_TABLE0_HOST  the iteration-0 tables come from the host through the kernel arguments instead
+//                    of being computed by every workgroup (~10 % of a low-p syndrome-stop launch)
+#ifndef QEC_TABLE0_HOST
+#define QEC_TABLE0_HOST 1
+#endif
 //   QEC_TRACK_FROM   first iteration whose var pass tests whether the sector became hard
 #ifndef QEC_TRACK_FROM
 #define QEC_TRACK_FROM 2
@@ -191,6 +196,7 @@ __device__ __forceinline__ bool all_live_sh(bool pred, bool live)
 __device__ __forceinline__ bool hard_ok(float pp) { return pp > 0.0f && pp < 1.0f; }
 
 constexpr int kMaxRL = 128;  // largest R*L a kernel argument block carries
+constexpr int kMaxTab0 = 448;  // iteration-0 table entries, (2^RX RX + 2^RZ RZ), of every instantiated variant
 constexpr int kMaxR = 16;
 constexpr int kMaxL = 32;
 
@@ -217,6 +223,9 @@ struct BpArgs {
     int maxIter, stop;
     int hardPaths;  // QEC_HP_* bits: hard-message paths / cycle jump (QEC_OPT_HARD_PATHS, QEC_OPT_CYCLE_JUMP)
     // lane-relabelled circulant tables (see relabel() below)
+    // iteration-0 tables of both sectors computed on the host (QEC_TABLE0_HOST: the same operations,
+    // so the same bits, as table0_entry on the device; each workgroup copies them to LDS)
+    float tab0[kMaxTab0];
     int SX[kMaxRL], SZ[kMaxRL];  // rotation of block (r, l) between check and variable views
     int DX[kMaxR], DZ[kMaxR];    // check-view lane lambda holds check (r, (lambda + D[r]) mod P)
     int CX[kMaxL], CZ[kMaxL];    // var-view lane mu holds variable (l, (mu + C[l]) mod P)
@@ -941,7 +950,7 @@ __device__ __forceinline__ bool iteration(const BpArgs& a, float (&msg)[R][L], u
 // would run (so the same bits), and iteration 0 becomes gathers of syndrome bits and table reads.
 // Not used when iteration 0 is the last one (N = 1: the self message is included).
 template <int R, int L>
-__device__ __forceinline__ float table0_entry(float pp, int e)
+__host__ __device__ inline float table0_entry(float pp, int e)
 {
     const float a = __builtin_fmaf(-2.0f, pp, 1.0f);  // 1.0f - 2.0f*q, as check_pass
     float t = 1.0f;
@@ -1370,8 +1379,13 @@ void bp_decode_kernel(const BpArgs a)
     __shared__ float tab0[QEC_TABLE0 ? kTabX + kTabZ : 1];
     if constexpr (QEC_TABLE0) {
         const float ppt = 2.0f / 3.0f * a.errorProbability;
-        for (int e = threadIdx.x; e < kTabX + kTabZ; e += blockDim.x)
-            tab0[e] = e < kTabX ? table0_entry<RX, L>(ppt, e) : table0_entry<RZ, L>(ppt, e - kTabX);
+        if constexpr (QEC_TABLE0_HOST && kTabX + kTabZ <= kMaxTab0) {
+            (void)ppt;
+            for (int e = threadIdx.x; e < kTabX + kTabZ; e += blockDim.x) tab0[e] = a.tab0[e];
+        } else {
+            for (int e = threadIdx.x; e < kTabX + kTabZ; e += blockDim.x)
+                tab0[e] = e < kTabX ? table0_entry<RX, L>(ppt, e) : table0_entry<RZ, L>(ppt, e - kTabX);
+        }
         __syncthreads();
     }
     // this wave's decision stage for packed records (emit_decisions)
@@ -1489,8 +1503,22 @@ struct Variant {
     KernelFn fn[3];     // indexed by stop rule
     KernelFn split[3];  // the same with one wave per sector (nullptr: not instantiated)
     KernelFn phase[3];  // QEC_OPT_PHASE_STATS: instrumented kernels (shipped codes only)
+    int (*fill_tab0)(float pp, float* out);  // host iteration-0 tables (QEC_TABLE0_HOST)
     const char* name;
 };
+
+// Both sectors' iteration-0 tables on the host, entry for entry what the device's table0_entry
+// computes (same IEEE fp32 operations, -ffp-contract=off); returns the entry count, 0 if they do
+// not fit the argument block.
+template <int J, int K, int L>
+static int fill_tab0(float pp, float* out)
+{
+    constexpr int tx = (1 << J) * J, tz = (1 << K) * K;
+    if (tx + tz > kMaxTab0) return 0;
+    for (int e = 0; e < tx; ++e) out[e] = table0_entry<J, L>(pp, e);
+    for (int e = 0; e < tz; ++e) out[tx + e] = table0_entry<K, L>(pp, e);
+    return tx + tz;
+}
 
 template <int J, int K, int L, class SH, class TU, bool WITH_SPLIT>
 static Variant make_variant(int P, int S, int T, const char* name)
@@ -1501,6 +1529,7 @@ static Variant make_variant(int P, int S, int T, const char* name)
                bp_decode_kernel<J, K, L, QEC_STOP_SYNDROME, SH, TU, false>},
               {nullptr, nullptr, nullptr},
               {nullptr, nullptr, nullptr},
+              fill_tab0<J, K, L>,
               name};
     if constexpr (WITH_SPLIT) {
         v.split[QEC_STOP_REF] = bp_decode_kernel<J, K, L, QEC_STOP_REF, SH, TU, true>;
@@ -1650,6 +1679,7 @@ int launch_decode(const void* variant, const Code& c, const uint8_t* sX, const u
     a.maxIter = maxIter < 0 ? 0 : maxIter;
     a.stop = stop;
     a.hardPaths = hardPaths & (QEC_HP_FORMS | QEC_HP_CYCLE);
+    if (QEC_TABLE0_HOST) v->fill_tab0(2.0f / 3.0f * errorProbability, a.tab0);  // p' as the kernel forms it
     relabel(c.EX.data(), c.J, c.L, c.P, v->relabel, a.SX, a.DX, a.CX);
     relabel(c.EZ.data(), c.K, c.L, c.P, v->relabel, a.SZ, a.DZ, a.CZ);
     const int wavesPerBlock = v->waves_per_block;

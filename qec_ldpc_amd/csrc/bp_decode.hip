@@ -1355,7 +1355,7 @@ __device__ __forceinline__ void decode_sector(const BpArgs& a, Lane& ln, uint32_
 
 // MINW: minimum waves per SIMD the register allocator must allow (5 -> <= 96 VGPRs), measured
 // per variant with tools/kbench (P61: 5 waves beat 4 by 4 %; see profiles/).
-// SPLIT: waves 2k and 2k+1 decode sectors X and Z of group k (adjacent waves, one workgroup);
+// SPLIT: waves 2k and 2k+1 decode sectors X and Z of group k (adjacent waves; they meet in a global merge word);
 // the launch zeroed flags[] and each sector ORs in its bits.  Otherwise one wave decodes both.
 template <class TU>
 constexpr int waves_per_block() { return QEC_WAVES_PER_BLOCK > 0 ? QEC_WAVES_PER_BLOCK : TU::kWavesPerBlock; }
@@ -1444,10 +1444,10 @@ using KernelFn = void (*)(const BpArgs);
 // P7's fixed and reference stops gain nothing, but its syndrome stop does (0.087 vs 0.100 ms)
 // (profiles/r01/session7/cmp_s7u_*.txt, cmp_s7v_*.txt).  So those kernels come from there.
 // A distinct Tune type keeps the two units' kernels apart (same code, different symbols).
-using TuneP61 = Tune<5, true, false, true, true, false, true, 1, 2, 4>;
+using TuneP61 = Tune<5, true, false, true, true, false, true, 1, 1, 4>;
 struct TuneP61MinReg : TuneP61 {};
 using ShiftsP61 = GeneratedShifts<4, 5, 10, 61, 9, 49, TuneP61::kRelabel, TuneP61::kMaskSelect>;
-using TuneP7 = Tune<8, true, false, true, true, true, false, 1, 4, 7>;
+using TuneP7 = Tune<8, true, false, true, true, true, false, 1, 1, 7>;
 struct TuneP7MinReg : TuneP7 {};
 using ShiftsP7 = GeneratedShifts<3, 3, 6, 7, 2, 3, TuneP7::kRelabel, TuneP7::kMaskSelect>;
 #ifndef QEC_P61_MINREG
@@ -1567,6 +1567,9 @@ static Variant gen()
 // the agreement test (kAgree) the syndrome-stop kernels are spill-free, P61 at 4 waves (125 VGPRs)
 // and P7 at 7 (with the lane relabelling and gather pipelining P7 now takes too, 2-5 % faster
 // at every stop rule: 260 instead of 456 static ds_bpermute; profiles/r02/p7_variants_r02s3{s,t}.txt).
+// With the iteration-0 tables from the host (QEC_TABLE0_HOST) nothing is shared between the waves
+// of a workgroup any more, and one-wave workgroups are fastest for both codes (P61 headline 134.0
+// vs 131.9M syn/s with two, P7 +3 % vs four; profiles/r02/cmp_wpb_r02s3x.txt).
 static Variant gen_p61()
 {
     Variant v = gen<4, 5, 10, 61, 9, 49, TuneP61>();

@@ -1444,10 +1444,10 @@ using KernelFn = void (*)(const BpArgs);
 // P7's fixed and reference stops gain nothing, but its syndrome stop does (0.087 vs 0.100 ms)
 // (profiles/r01/session7/cmp_s7u_*.txt, cmp_s7v_*.txt).  So those kernels come from there.
 // A distinct Tune type keeps the two units' kernels apart (same code, different symbols).
-using TuneP61 = Tune<5, true, false, true, true, false, true, 1, 1, 4>;
+using TuneP61 = Tune<5, true, false, true, true, false, true, 2, 1, 4>;
 struct TuneP61MinReg : TuneP61 {};
 using ShiftsP61 = GeneratedShifts<4, 5, 10, 61, 9, 49, TuneP61::kRelabel, TuneP61::kMaskSelect>;
-using TuneP7 = Tune<8, true, false, true, true, true, false, 1, 1, 7>;
+using TuneP7 = Tune<8, true, false, true, true, true, false, 2, 1, 7>;
 struct TuneP7MinReg : TuneP7 {};
 using ShiftsP7 = GeneratedShifts<3, 3, 6, 7, 2, 3, TuneP7::kRelabel, TuneP7::kMaskSelect>;
 #ifndef QEC_P61_MINREG

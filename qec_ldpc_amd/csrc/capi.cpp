@@ -453,8 +453,14 @@ namespace {
 // removes stays about one long sector (~0.1 ms); P61 at 2^20: 118.7 M/s unordered vs 116.9 M/s,
 // at 131 072: 101 M/s vs 113 M/s (profiles/r02/ab_schedule.txt).  Several syndromes per wave (P7)
 // always gain: similar syndromes then share waves (1.56 G/s vs 0.88 G/s at 2^20).
+// Under the syndrome stop at low p nearly every sector stops at iteration 0 or 1, so there is no
+// tail to remove and the pass is pure cost: below kScheduleSyndromeMinP it stays off there
+// (P61, 65 536 per batch: p = 0.001 290 vs 266 M/s, 0.002 263 vs 257 off vs on, but 0.005 190 vs
+// 197, 0.01 124 vs 143; 262 144 at p = 0.002: 0.450 vs 0.521 ms; profiles/r02/psweep_sched{0,1}_r02s3g.json,
+// profiles/r02/cmp_options_r02s3zb.txt).
 constexpr long long kScheduleMinBatch = 4096;
 constexpr long long kScheduleMaxSingle = 1LL << 19;
+constexpr float kScheduleSyndromeMinP = 0.004f;
 
 // One decode launch of a single-device handle on device buffers.  Outputs: byte form (eX, eZ,
 // flags) or, with rec non-null, the packed decision records.
@@ -488,7 +494,8 @@ int dispatch_decode(qec_decoder* d, const uint8_t* sX, const uint8_t* sZ, long l
     const int32_t* perm = nullptr;
     bool zeroed = false;
     const bool single = 2 * c.P > 64;  // one syndrome per wave
-    const bool auto_on = B >= kScheduleMinBatch && (!single || B <= kScheduleMaxSingle);
+    const bool auto_on = B >= kScheduleMinBatch && (!single || B <= kScheduleMaxSingle) &&
+                         !(stop == QEC_STOP_SYNDROME && p < kScheduleSyndromeMinP);
     if (B > 1 && B <= schedule_max_batch() && (d->schedule == 2 || (d->schedule == 1 && auto_on))) {
         if ((rc = ws_reserve(d->sched, schedule_workspace_bytes(B, c.mX, c.mZ), st, "decode: dispatch order")))
             return rc;

@@ -497,7 +497,7 @@ class DecoderGPU:
                                             ctypes.c_void_p(self._stream(stream))), "qec_pack_decisions_dev")
 
     # ---- Monte-Carlo ---------------------------------------------------------------------
-    def monte_carlo(self, seed, start, count, p, max_iter, stop="syndrome", batch=65536):
+    def monte_carlo(self, seed, start, count, p, max_iter, stop="syndrome", batch=1 << 20):
         """Device Monte-Carlo run (sample -> syndrome -> decode -> statistics); returns a dict."""
         r = MCResult()
         _check(lib().qec_monte_carlo(self._h, seed & (2 ** 64 - 1), start, count, float(p), int(max_iter),

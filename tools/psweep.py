@@ -46,7 +46,9 @@ def main():
     ap.add_argument("--ps", type=float, nargs="*", default=DEFAULT_PS)
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--stop", default="syndrome", choices=["syndrome", "ref", "fixed"])
-    ap.add_argument("--batch", type=int, default=65536)
+    # one batch per p per GPU: batches of 65 536 ran 25-35 % slower (five launches and their gaps
+    # per batch, and a launch tail each; profiles/r02/psweep_batch_r02s3zd.json)
+    ap.add_argument("--batch", type=int, default=1 << 20)
     ap.add_argument("--seed", type=lambda v: int(v, 0), default=0x51EC0DE)
     ap.add_argument("--out", default=None, help="write the per-p lines to this JSON file (rank 0)")
     ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
@@ -73,7 +75,8 @@ def main():
         k, v = kv.split("=")
         dec.set_option(k, int(v))
     lo, hi = shard_range(args.total, rank, world)
-    dec.monte_carlo(args.seed, lo, min(hi - lo, 4096), args.ps[0], args.iters, args.stop, args.batch)  # warm-up
+    # warm-up at the full batch size, so the workspace is reserved before the timed runs
+    dec.monte_carlo(args.seed, lo, min(hi - lo, args.batch), args.ps[0], args.iters, args.stop, args.batch)
     lines = []
     for p in args.ps:
         if world > 1:

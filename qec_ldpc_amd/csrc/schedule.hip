@@ -220,7 +220,10 @@ int launch_schedule(const uint8_t* sX, const uint8_t* sZ, bool sbits, long long 
     if (B > schedule_max_batch()) return fail(QEC_ERR_ARG, "schedule: batch too large to order");
     const bool shortrows = sbits || mX + mZ <= kShortRows;
     int nch = 0;
-    const int chunk = chunk_of(B, shortrows ? kHistThreads : 256, &nch);
+    // short rows: 4096 syndromes per chunk (four per thread): the offsets and scatter passes then
+    // handle a quarter of the chunks (P7 2^20: order pass 60 -> 51 us, profiles/r02/hist_ab_r02s3zj.txt;
+    // staging the rows through LDS did not speed the histogram up)
+    const int chunk = chunk_of(B, shortrows ? 4 * kHistThreads : 256, &nch);
     uint8_t* p = static_cast<uint8_t*>(ws);
     int32_t* perm = reinterpret_cast<int32_t*>(p);
     uint32_t* counts = reinterpret_cast<uint32_t*>(p + perm_bytes(B));

@@ -680,15 +680,22 @@ int launch_sample_depolarizing(uint64_t seed, uint64_t start, long long B, int n
 
 static uint32_t magic_of(long long d) { return d > 1 ? (uint32_t)(((1ull << 32) + (uint64_t)d - 1) / (uint64_t)d) : 0u; }
 
-// samples per wave of mc_gap_kernel (QEC_GAP_SPW overrides, for experiments)
-static int gap_spw_default()
+// samples per wave of mc_gap_kernel: as many as keep ~8 waves per SIMD busy (8 192 waves), between
+// 16 and 64 -- a wave's walk lasts as long as its busiest lane, so more samples per wave cost less
+// per sample once there are enough waves (P61, 2^20 samples: 206 / 126 / 124 us at 16 / 32 / 64 per
+// wave at p = 0.002, 1109 / 542 us at 16 / 64 at p = 0.05; 65 536 samples: 16 best, 20 vs 22 us at
+// 64; profiles/r02/gap_spw_r02s3zn.txt).  QEC_GAP_SPW overrides, for experiments.
+static int gap_spw(long long B)
 {
     static const int v = [] {
         const char* e = std::getenv("QEC_GAP_SPW");
         const int k = e ? std::atoi(e) : 0;
-        return k >= 1 && k <= 64 ? k : 16;
+        return k >= 1 && k <= 64 ? k : 0;
     }();
-    return v;
+    if (v) return v;
+    int spw = 16;
+    while (spw < 64 && B / (2 * spw) >= 8192) spw *= 2;
+    return spw;
 }
 
 static int launch_mc_gap(const McArgsHost& h, hipStream_t st)
@@ -718,7 +725,7 @@ static int launch_mc_gap(const McArgsHost& h, hipStream_t st)
     a.w32 = a.ew + a.wX + a.wZ;
     a.estride = h.errp_words ? 4 * a.ew : 2 * a.nb;
     // at most 16 KiB of sample state per wave
-    a.spw = std::max(1, std::min(gap_spw_default(), 16384 / (4 * a.w32)));
+    a.spw = std::max(1, std::min(gap_spw(h.B), 16384 / (4 * a.w32)));
     if ((long long)a.spw * std::max<long long>({(long long)c.mX, (long long)c.mZ, 2LL * a.nb}) >= 65536)
         return fail(QEC_ERR_UNSUPPORTED, "mc front end: code too long");
     a.magicX = magic_of(c.mX); a.magicZ = magic_of(c.mZ); a.magicE = magic_of(2 * a.nb);

@@ -50,6 +50,7 @@ def main():
     # per batch, and a launch tail each; profiles/r02/psweep_batch_r02s3zd.json)
     ap.add_argument("--batch", type=int, default=1 << 20)
     ap.add_argument("--seed", type=lambda v: int(v, 0), default=0x51EC0DE)
+    ap.add_argument("--reps", type=int, default=3, help="runs per p (the fastest is reported)")
     ap.add_argument("--out", default=None, help="write the per-p lines to this JSON file (rank 0)")
     ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
                     help="decoder option (qec_decoder_set_option), e.g. schedule=0")
@@ -81,9 +82,16 @@ def main():
     for p in args.ps:
         if world > 1:
             dist.barrier()
-        t0 = time.perf_counter()
-        r = dec.monte_carlo(args.seed, lo, hi - lo, p, args.iters, args.stop, args.batch)
-        dt = time.perf_counter() - t0
+        # the same samples --reps times (identical counters); the fastest run's time, so one host
+        # hiccup of a few ms does not stand for a 2-10 ms sweep point
+        dt = None
+        for _ in range(max(1, args.reps)):
+            t0 = time.perf_counter()
+            r = dec.monte_carlo(args.seed, lo, hi - lo, p, args.iters, args.stop, args.batch)
+            t = time.perf_counter() - t0
+            if dt is None or t < dt:
+                dt, best = t, r
+        r = best
         vec = torch.tensor([r[k] for k in FIELDS], dtype=torch.int64, device=dev)
         tm = torch.tensor([dt, r["decodeSeconds"]], dtype=torch.float64, device=dev)
         if world > 1:

@@ -206,6 +206,25 @@ def test_fused_front_end(env, key, seed, start, p):
     assert np.array_equal(errp.cpu().numpy(), exp)
 
 
+@pytest.mark.parametrize("key", ["P7", "P61"])
+def test_fused_front_end_wave_width(env, key):
+    """The front end's samples per wave grow with the batch (16 .. 64 lanes, montecarlo.hip
+    gap_spw); the samples do not depend on it: a 2^18-sample launch (64 per wave) equals the
+    numpy restatement on a slice and a 1000-sample launch (16 per wave) of the same indices."""
+    code, dec, _ = env[key]
+    B, lo, seed, p = 1 << 18, 123456, 99, 0.02
+    big = [u8(B, code.numEqsX), u8(B, code.numEqsZ), u8(B, 2 * ((code.n + 7) // 8))]
+    dec.sample_syndrome_dev(seed, 0, p, *big)
+    small = [u8(1000, code.numEqsX), u8(1000, code.numEqsZ), u8(1000, 2 * ((code.n + 7) // 8))]
+    dec.sample_syndrome_dev(seed, lo, p, *small)
+    torch.cuda.synchronize()
+    for a, b in zip(big, small):
+        assert torch.equal(a[lo:lo + 1000], b)
+    x, z = depolarizing(seed, lo, 1000, code.n, p)
+    assert np.array_equal(small[0].cpu().numpy(), code.syndrome(0, x))
+    assert np.array_equal(small[1].cpu().numpy(), code.syndrome(1, z))
+
+
 @pytest.mark.parametrize("key,B,p,N", [("P7", 4000, 0.06, 30), ("P61", 500, 0.03, 30)])
 def test_statistics_packed_equals_byte_form(env, key, B, p, N):
     code, dec, _ = env[key]

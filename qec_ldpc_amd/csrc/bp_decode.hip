@@ -1453,6 +1453,9 @@ using ShiftsP7 = GeneratedShifts<3, 3, 6, 7, 2, 3, TuneP7::kRelabel, TuneP7::kMa
 #ifndef QEC_P61_MINREG
 #define QEC_P61_MINREG 1
 #endif
+#ifndef QEC_P61_SYN_MINREG
+#define QEC_P61_SYN_MINREG 0  // the P61 syndrome-stop kernels from the minreg unit too
+#endif
 KernelFn p61_minreg_kernel(int stop, bool split);  // bp_decode_p61.hip
 KernelFn p7_minreg_kernel(int stop, bool split);   // bp_decode_p61.hip
 
@@ -1467,6 +1470,11 @@ KernelFn p61_minreg_kernel(int stop, bool split)
     if (stop == QEC_STOP_FIXED)
         return split ? bp_decode_kernel<4, 5, 10, QEC_STOP_FIXED, ShiftsP61, TuneP61MinReg, true>
                      : bp_decode_kernel<4, 5, 10, QEC_STOP_FIXED, ShiftsP61, TuneP61MinReg, false>;
+#if QEC_P61_SYN_MINREG
+    if (stop == QEC_STOP_SYNDROME)
+        return split ? bp_decode_kernel<4, 5, 10, QEC_STOP_SYNDROME, ShiftsP61, TuneP61MinReg, true>
+                     : bp_decode_kernel<4, 5, 10, QEC_STOP_SYNDROME, ShiftsP61, TuneP61MinReg, false>;
+#endif
     return nullptr;
 }
 KernelFn p7_minreg_kernel(int stop, bool split)
@@ -1575,7 +1583,8 @@ static Variant gen_p61()
     Variant v = gen<4, 5, 10, 61, 9, 49, TuneP61>();
     for (int stop : {QEC_STOP_REF, QEC_STOP_FIXED, QEC_STOP_SYNDROME}) v.phase[stop] = phase_kernel(61, stop);
     if (QEC_P61_MINREG) {
-        for (int stop : {QEC_STOP_REF, QEC_STOP_FIXED}) {
+        for (int stop : {QEC_STOP_REF, QEC_STOP_FIXED, QEC_STOP_SYNDROME}) {
+            if (stop == QEC_STOP_SYNDROME && !QEC_P61_SYN_MINREG) continue;
             v.fn[stop] = p61_minreg_kernel(stop, false);
             v.split[stop] = p61_minreg_kernel(stop, true);
         }

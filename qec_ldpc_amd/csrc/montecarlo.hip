@@ -454,7 +454,6 @@ struct GapArgs {
     uint8_t* errp;     // nullable
     const int32_t* varEdge;  // non-QC codes: n x dvX then n x dvZ edge ids; check = edge / dc
     int dc, dvX, dvZ;
-    int ablate;              // timing experiments only (QEC_GAP_ABLATE; wrong outputs): 1 no write-out, 2 no walk
     int EX[128], EZ[128];    // QC codes
 };
 
@@ -501,7 +500,7 @@ __global__ __launch_bounds__(64 * kGapWaves) void mc_gap_kernel(const GapArgs a)
     if (b0 >= a.B) return;  // wave-local from here on
     const int ns = (int)(a.B - b0 < a.spw ? a.B - b0 : a.spw);
     const int w32 = a.w32, ew = a.ew, wX = a.wX, wZ = a.wZ;
-    if (lane < ns && a.gp.thr != 0 && a.ablate != 2) {
+    if (lane < ns && a.gp.thr != 0) {
         uint32_t* __restrict__ mine = reg + lane * w32;
         uint32_t* __restrict__ synX = mine + ew;
         uint32_t* __restrict__ synZ = synX + wX;
@@ -541,7 +540,6 @@ __global__ __launch_bounds__(64 * kGapWaves) void mc_gap_kernel(const GapArgs a)
         });
     }
     wave_sync();
-    if (a.ablate == 1) return;
     if (a.sXp != nullptr) {
         write_words(a.sXp + b0 * wX, ns * wX, lane, [&](int k) {
             const int s = qdiv(k, a.magicWX);
@@ -709,10 +707,6 @@ static int launch_mc_gap(const McArgsHost& h, hipStream_t st)
     a.sX = h.sX; a.sZ = h.sZ; a.sXp = h.sXp; a.sZp = h.sZp; a.errp = h.errp;
     a.varEdge = h.varEdge;
     a.dc = c.L; a.dvX = c.J; a.dvZ = c.K;
-    {
-        static const int ab = [] { const char* e = std::getenv("QEC_GAP_ABLATE"); return e ? std::atoi(e) : 0; }();
-        a.ablate = ab;
-    }
     if (a.varEdge == nullptr) {
         if (!c.is_qc || c.J * c.L > 128 || c.K * c.L > 128)
             return fail(QEC_ERR_UNSUPPORTED, "mc front end: needs a QC code or a check table");

@@ -184,7 +184,7 @@ __device__ __forceinline__ bool logical_from_columns(const unsigned long long* r
 // Grid-stride over samples, one wave per sample at a time; each wave keeps its counts in
 // registers and the workgroup adds them to `counters` once (same-address atomics from every
 // workgroup serialise at L2: 16 384 four-wave workgroups x 8 counters cost ~190 us per 65 536
-// samples, profiles/r02/mc_r02f_trace.csv).
+// samples, profiles/r02/mc_r02f_psweep_p002_kernel_stats.csv).
 constexpr int kStatBlockWaves = 16;
 constexpr int kStatMaxBlocks = 256;
 

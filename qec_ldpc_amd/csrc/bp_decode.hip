@@ -1646,10 +1646,16 @@ const void* select_variant(const Code& c, std::string& name)
 
 // QEC_OPT_SECTOR_SPLIT: 0 off, 1 the variant's tuned choice, 2 on (runtime-shift variants have
 // no split kernels: one wave per syndrome)
-bool decode_uses_split(const void* variant, int stop, int split)
+// The tuned choice (split_auto) splits only batches below kSplitAutoMaxBatch: the two waves per
+// syndrome group help fill the chip when waves are few, and cost a merge per syndrome when they are
+// not (P7 fixed 20: 65 536 616 vs 512 M/s, 131 072 992 vs 846, 262 144 even, 524 288 1613 vs 1643,
+// 2^20 1790 vs 1835 M/s split vs one wave per group; profiles/r02/p7_split_r02s3zz.txt).
+constexpr long long kSplitAutoMaxBatch = 1LL << 19;
+
+bool decode_uses_split(const void* variant, int stop, int split, long long B)
 {
     const Variant* v = static_cast<const Variant*>(variant);
-    return (split == 2 || (split == 1 && v->split_auto)) && v->split[stop] != nullptr;
+    return (split == 2 || (split == 1 && v->split_auto && B < kSplitAutoMaxBatch)) && v->split[stop] != nullptr;
 }
 
 bool decode_has_phase_stats(const void* variant, int stop)
@@ -1675,7 +1681,7 @@ int launch_decode(const void* variant, const Code& c, const uint8_t* sX, const u
     const bool phase = (hardPaths & QEC_HP_PHASE) != 0;
     if (phase && v->phase[stop] == nullptr)
         return fail(QEC_ERR_UNSUPPORTED, "bp_decode: no phase-statistics kernel for this code");
-    split = !phase && decode_uses_split(variant, stop, split) && merge != nullptr;
+    split = !phase && decode_uses_split(variant, stop, split, B) && merge != nullptr;
     if (split) {
         a.merge = merge;
         if (!merge_zeroed && hipMemsetAsync(merge, 0, (size_t)B * sizeof(uint32_t), stream) != hipSuccess)

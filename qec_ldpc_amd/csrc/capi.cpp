@@ -23,7 +23,7 @@ size_t schedule_workspace_bytes(long long B, int mX, int mZ);
 long long schedule_max_batch();
 int launch_schedule(const uint8_t* sX, const uint8_t* sZ, bool sbits, long long B, int mX, int mZ, void* ws,
                     uint32_t* zero_merge, int32_t** perm_out, hipStream_t st);
-bool decode_uses_split(const void* variant, int stop, int split);
+bool decode_uses_split(const void* variant, int stop, int split, long long B);
 bool decode_has_phase_stats(const void* variant, int stop);
 int launch_sample_depolarizing(uint64_t seed, uint64_t start, long long B, int n, float p, uint8_t* x, uint8_t* z,
                                hipStream_t st);
@@ -489,7 +489,7 @@ int dispatch_decode(qec_decoder* d, const uint8_t* sX, const uint8_t* sZ, long l
     }
     const int hp = (d->hard_paths ? (QEC_HP_FORMS | (d->cycle_jump ? QEC_HP_CYCLE : 0)) : 0) |
                    (d->phase_stats ? QEC_HP_PHASE : 0);
-    const bool split = !d->phase_stats && decode_uses_split(d->variant, stop, d->sector_split);
+    const bool split = !d->phase_stats && decode_uses_split(d->variant, stop, d->sector_split, B);
     if (split && (rc = ws_reserve(d->merge, (size_t)B, st, "decode"))) return rc;
     const int32_t* perm = nullptr;
     bool zeroed = false;

@@ -7,7 +7,7 @@ HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -fno-f
 CSRC     := qec_ldpc_amd/csrc
 OBJ      := build/obj
 LIB      := qec_ldpc_amd/libqecldpc.so
-OBJS     := $(OBJ)/bp_decode.o $(OBJ)/bp_decode_p61.o $(OBJ)/bp_decode_phase.o $(OBJ)/bp_sparse.o $(OBJ)/schedule.o $(OBJ)/montecarlo.o $(OBJ)/code_model.o $(OBJ)/cpu_engine.o $(OBJ)/capi.o
+OBJS     := $(OBJ)/bp_decode.o $(OBJ)/bp_decode_p61.o $(OBJ)/bp_decode_phase.o $(OBJ)/bp_sparse.o $(OBJ)/schedule.o $(OBJ)/triage.o $(OBJ)/montecarlo.o $(OBJ)/code_model.o $(OBJ)/cpu_engine.o $(OBJ)/capi.o
 HDRS     := include/qec_ldpc.h include/HostDeviceArray.h $(CSRC)/qec_internal.h $(CSRC)/qec_device.h
 
 all: $(LIB) oracle tools/qec_ldpc tools/getstats_check
@@ -30,6 +30,9 @@ $(OBJ)/bp_sparse.o: $(CSRC)/bp_sparse.hip $(HDRS) | $(OBJ)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(OBJ)/schedule.o: $(CSRC)/schedule.hip $(HDRS) | $(OBJ)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(OBJ)/triage.o: $(CSRC)/triage.hip $(HDRS) | $(OBJ)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(OBJ)/montecarlo.o: $(CSRC)/montecarlo.hip $(HDRS) | $(OBJ)

@@ -26,6 +26,13 @@ Prints one JSON line (rank 0).  Extra objects:
                   iterations executed" rate.
   sector_iterations  executed sector-iterations of one launch by phase (soft / hard / agreed /
                   jumped), from the instrumented kernel (QEC_OPT_PHASE_STATS).
+  executed_iteration_fraction  executed / nominal sector-iterations of the timed launch (the rest are
+                  exact jumps; 1.0 for value_full_arithmetic).
+  ref_stop        the same batch under the reference stop rule (DecoderCPU::Decode unmodified): rate,
+                  per-sector iteration histogram, oracle check on a slice.
+  published_blocks  DecoderGPU::GetStatistics on two of the reference's published results blocks
+                  (seeded MSVC sampler, same samples): rate vs the published duration, counters checked,
+                  on one decoder and on a two-part (multi-device API) decoder.
   sustained       a >= 1 s window of the same step (clock-settled rate).
   cpu_baseline    the oracle (CPU restatement of DecoderCPU, OpenMP) on host cores, rank 0 at
                   N = 1 only, bounded sample of the same workload; also 1 thread and
@@ -85,17 +92,34 @@ def shard(total, rank, world):
     return total * rank // world, total * (rank + 1) // world
 
 
-def load_pmc(code_name, iters, stop, p):
-    """profiles/pmc_<code>.json if it was collected on this workload (code, iters, stop, p)."""
-    path = os.path.join(ROOT, "profiles", "pmc_%s.json" % code_name)
-    try:
-        with open(path) as f:
-            pm = json.load(f)
-    except (OSError, ValueError):
-        return None, path
-    if pm.get("iters") != iters or pm.get("stop") != stop or abs(float(pm.get("p", -1)) - p) > 1e-12:
-        return None, path
-    return pm, path
+def library_sha256():
+    import hashlib
+    with open(os.path.join(ROOT, "qec_ldpc_amd", "libqecldpc.so"), "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()
+
+
+def load_pmc(code_name, iters, stop, p, batch):
+    """profiles/pmc_<code>_<batch>.json or profiles/pmc_<code>.json if it was collected on this
+    workload (code, iters, stop, p, batch) with this very library (tools/gpu/pmc_summary.py stamps
+    the library's sha256): a profile of another binary or batch would mis-state the roofline."""
+    why = []
+    lib = library_sha256()
+    for name in ("pmc_%s_%d.json" % (code_name, batch), "pmc_%s.json" % code_name):
+        path = os.path.join(ROOT, "profiles", name)
+        try:
+            with open(path) as f:
+                pm = json.load(f)
+        except (OSError, ValueError):
+            continue
+        if pm.get("iters") != iters or pm.get("stop") != stop or abs(float(pm.get("p", -1)) - p) > 1e-12:
+            why.append("%s: other workload" % name)
+        elif pm.get("batch") != batch:
+            why.append("%s: batch %s" % (name, pm.get("batch")))
+        elif pm.get("library_sha256") != lib:
+            why.append("%s: collected on another build of the library" % name)
+        else:
+            return pm, path
+    return None, "; ".join(why) or "no profiles/pmc_%s*.json" % code_name
 
 
 def main():
@@ -240,7 +264,7 @@ def main():
         "mean_iterations": {"X": round(it_mean[0], 4), "Z": round(it_mean[1], 4)},
         "decode_ms": round(kernel_ms, 4),
     }
-    pm, pm_path = load_pmc(args.code, iters, args.stop, p)
+    pm, pm_path = load_pmc(args.code, iters, args.stop, p, B)
     out["roofline"] = valu_roofline(pm, pm_path, B, kernel_ms, args.hard_paths)
     ab = algorithmic_bytes_per_syndrome(code, it_mean[0], it_mean[1]) * B
     gbs = ab / (kernel_ms * 1e-3) / 1e9
@@ -252,17 +276,22 @@ def main():
 
     if not args.no_extras:
         if args.hard_paths:
-            full = retime(dec, step, stream, B, outs, {"hard_paths": 0})
-            # whole job: every rank decodes an equal shard at this rank's rate
-            out["value_full_arithmetic"] = round(full["syndromes_per_s"] * world, 1)
+            full = retime(dec, step, stream, B, outs, {"hard_paths": 0}, world=world)
+            # whole job: every rank's shard at the slowest rank's kernel time
+            out["value_full_arithmetic"] = full["syndromes_per_s"]
             ops = lane_ops_per_syndrome(code, 1) * (it_mean[0] + it_mean[1]) / 2.0
             tops = ops * B / (full["kernel_ms"] * 1e-3) / 1e12
             full["valu_lane_ops"] = {"achieved": round(tops, 2), "peak": VALU_PEAK_TOPS, "unit": "Tlane-op/s",
                                      "frac": round(tops / VALU_PEAK_TOPS, 4),
                                      "basis": "analytical lane-ops of full-arithmetic BP (DESIGN.md section 5)"}
             out["full_arithmetic"] = full
-            out["no_cycle_jump"] = retime(dec, step, stream, B, outs, {"cycle_jump": 0})
+            out["no_cycle_jump"] = retime(dec, step, stream, B, outs, {"cycle_jump": 0}, world=world)
         out["sector_iterations"] = phase_counts(dec, step, stream, its, B)
+        pl = out["sector_iterations"].get("per_launch")
+        if pl:
+            out["executed_iteration_fraction"] = round(pl["sector_iterations_executed"] / pl["sector_iterations_nominal"], 4)
+        if args.stop == "fixed" and packed:
+            out["ref_stop"] = ref_stop(dec, sX, sZ, p, iters, B, stream, world, fname, rank == 0 and not args.no_cpu)
         out["sustained"] = sustained(step, stream, dev, world, ms_per_step, args.min_seconds,
                                      global_batch if scaling == "strong" else B * world)
 
@@ -274,6 +303,8 @@ def main():
 
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(code, fname, sX, sZ, p, iters, args, outs, packed)
+    if rank == 0 and world == 1 and not args.no_extras:
+        out["published_blocks"] = published_blocks(local)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
@@ -317,7 +348,7 @@ def valu_roofline(pm, path, B, kernel_ms, hard_paths):
             "peak_basis": "1024 SIMDs x 2.4 GHz / 2 cycles per wave64 VALU instruction"}
     if pm is None or "valu_insts_per_syndrome" not in pm or not hard_paths:
         base.update({"achieved": None, "frac": None, "traffic": None,
-                     "note": "no PMC profile for this workload (%s)" % os.path.relpath(path, ROOT)})
+                     "note": "no PMC profile for this workload and library (%s)" % path})
         return base
     insts = pm["valu_insts_per_syndrome"] * B
     ach = insts / (kernel_ms * 1e-3) / 1e12
@@ -329,10 +360,12 @@ def valu_roofline(pm, path, B, kernel_ms, hard_paths):
     return base
 
 
-def retime(dec, step, stream, B, outs, opts, reps=3):
+def retime(dec, step, stream, B, outs, opts, reps=3, world=1):
     """Re-time the step with decoder options changed (e.g. hard_paths 0: every iteration in full
-    arithmetic) and check the outputs are the same bits."""
+    arithmetic) and check the outputs are the same bits.  At N > 1 the kernel time is the max over
+    ranks (as timed_steps) and the rate is the whole job's."""
     import torch
+    import torch.distributed as dist
     ref = [t.clone() for t in outs]
     old = {k: dec.get_option(k) for k in opts}
     for k, v in opts.items():
@@ -352,7 +385,11 @@ def retime(dec, step, stream, B, outs, opts, reps=3):
             dec.set_option(k, v)
     same = all(torch.equal(r, t) for r, t in zip(ref, outs))
     k = float(np.median(ms))
-    return {"kernel_ms": round(k, 4), "syndromes_per_s": round(B / k * 1e3, 1), "identical": bool(same)}
+    if world > 1:
+        t = torch.tensor([k, 0.0 if same else 1.0], dtype=torch.float64, device=outs[0].device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        k, same = float(t[0]), float(t[1]) == 0.0
+    return {"kernel_ms": round(k, 4), "syndromes_per_s": round(B * world / k * 1e3, 1), "identical": bool(same)}
 
 
 def phase_counts(dec, step, stream, its, B):
@@ -421,11 +458,107 @@ def gather_measure(dec, step, rec, B, world, rank, dev, stream, steps, global_ba
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     g, e = float(t[0]), float(t[1])
     nbytes = B * rec.shape[1]
-    return {"backend": backend, "record_bytes": int(rec.shape[1]), "bytes_per_rank": int(nbytes),
+    coll = "RCCL" if backend == "nccl" else backend
+    rccl = None
+    if backend == "nccl":
+        try:
+            v = torch.cuda.nccl.version()
+            rccl = ".".join(str(x) for x in v) if isinstance(v, tuple) else str(v)
+        except Exception:  # noqa: BLE001
+            rccl = None
+    return {"backend": backend, "backend_reported": dist.get_backend(), "world_size": dist.get_world_size(),
+            "rccl_version": rccl, "record_bytes": int(rec.shape[1]), "bytes_per_rank": int(nbytes),
             "gather_ms": round(g * 1e3, 4), "root_GBps": round(world * nbytes / g / 1e9, 2),
             "end_to_end": {"ms_per_step": round(e * 1e3, 4), "syndromes_per_s": round(global_batch / e, 1),
-                           "what": "packed decode of every shard + RCCL gather of all records to rank 0"},
+                           "what": "packed decode of every shard + %s gather of all records to rank 0" % coll},
             "rank0_shard_intact": ok}
+
+
+def ref_stop(dec, sX, sZ, p, iters, B, stream, world, fname, check):
+    """BASELINE.md section 3: the same resident batch under the reference stop rule (DecoderCPU::Decode
+    unmodified, QEC_LDPC/DecoderCPU.h:280-291): rate, per-sector iteration histogram, and on rank 0
+    the oracle's answers on a slice."""
+    import torch
+    import torch.distributed as dist
+    rec = torch.empty((B, dec.record_bytes()), dtype=torch.uint8, device=sX.device)
+    its = torch.empty((B, 2), dtype=torch.int32, device=sX.device)
+
+    def step():
+        dec.decode_batch_packed_dev(sX, sZ, p, iters, "ref", rec, its, stream=stream)
+
+    step()
+    torch.cuda.synchronize()
+    ms = []
+    for _ in range(5):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        step()
+        b.record(stream)
+        torch.cuda.synchronize()
+        ms.append(a.elapsed_time(b))
+    k = float(np.median(ms))
+    it = its.cpu().numpy()
+    if world > 1:
+        t = torch.tensor([k], dtype=torch.float64, device=sX.device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        k = float(t[0])
+    hist = {sec: {str(v): int(c) for v, c in enumerate(np.bincount(it[:, j])) if c}
+            for j, sec in enumerate(("X", "Z"))}
+    out = {"syndromes_per_s": round(B * world / k * 1e3, 1), "kernel_ms": round(k, 4), "cap": iters,
+           "iterations_hist_rank0": hist, "mean_iterations": {"X": round(float(it[:, 0].mean()), 4),
+                                                              "Z": round(float(it[:, 1].mean()), 4)}}
+    if check:
+        from oracle.oracle import OracleCode
+        from qec_ldpc_amd.codes import code_path
+        from qec_ldpc_amd.gather import unpack_records
+        n = min(B, 4096)
+        o = OracleCode(code_path(fname)).decode_batch(sX[:n].cpu().numpy(), sZ[:n].cpu().numpy(), p, iters, "ref")
+        gX, gZ, gF = unpack_records(rec[:n].cpu().numpy(), dec.code.n)
+        out["gpu_matches_oracle_on_sample"] = bool(np.array_equal(o[0], gX) and np.array_equal(o[1], gZ)
+                                                   and np.array_equal(o[2], gF) and np.array_equal(o[3], it[:n]))
+        out["oracle_sample"] = n
+    return out
+
+
+# The reference's published results blocks timed here (seed and counters from tests/golden/kat.json,
+# extracted from QEC_LDPC/results/**): the P61 block of init.txt (code610, W=15, 100 000 samples,
+# MAX 100, p 0.01: 112.73 s, results/[J=4,K=5,L=10,P=61,s=9,t=49][[n=610,k=61]]_W_15_MAX_100_p_0.01.txt:1-4)
+# and the P7 W=3 MAX 100 p 0.02 block (results/[2,3,6,7,2,3]/..._W_3_MAX_100_p_0.02.txt:1-4).
+PUBLISHED = [("J_4_K_5_L_10_P_61_s_9_t_49", 15, 100, 2287037912), ("J_3_K_3_L_6_P_7_s_2_t_3", 3, 100, 2596423950)]
+KAT_FIELDS = {"tested": "numErrorsTested", "withX": "numXErrorsTested", "withZ": "numZErrorsTested",
+              "corrected": "corrected", "synX": "syndromeErrorsX", "synZ": "syndromeErrorsZ",
+              "logical": "logicalErrors", "convX": "convergenceFailX", "convZ": "convergenceFailZ"}
+
+
+def published_blocks(device):
+    """DecoderGPU::GetStatistics (QEC_LDPC/main.cu:101's call, the reference's seeded VS2015 sampler
+    on the host, decode + I-P check on the GPU) on the published blocks: samples/s against the
+    block's own Duration, every counter compared; one decoder and a two-part decoder on this GPU."""
+    import qec_ldpc_amd as q
+    from qec_ldpc_amd.codes import code_path
+    with open(os.path.join(ROOT, "tests", "golden", "kat.json")) as f:
+        kat = json.load(f)
+    out = []
+    for fname, W, MAX, seed in PUBLISHED:
+        rec = next(r for r in kat if r["code"] == fname and r["W"] == W and r["MAX"] == MAX and r["seed"] == seed)
+        code = q.Quantum_LDPC_Code.createFromFile(code_path(fname))
+        line = {"block": "%s block %d" % (rec["file"], rec["block"]), "W": W, "MAX": MAX, "p": rec["p_run"],
+                "seed": seed, "samples": rec["tested"],
+                "reference": {"seconds": rec["duration_us"] / 1e6,
+                              "samples_per_s": round(rec["tested"] / (rec["duration_us"] / 1e6), 1),
+                              "hardware": "Intel i7-4720HQ, 8 OpenMP threads (SURVEY.md section 6)"}}
+        for label, devs in (("one_decoder", None), ("two_part_decoder", [device, device])):
+            dec = q.DecoderGPU(code, device) if devs is None else q.DecoderGPU(code, devices=devs)
+            dec.GetStatistics(W, 2000, rec["p_run"], MAX, seed)  # warm-up (workspace, code upload)
+            t = time.perf_counter()
+            st = dec.GetStatistics(W, rec["tested"], rec["p_run"], MAX, seed)
+            dt = time.perf_counter() - t
+            line[label] = {"seconds": round(dt, 4), "samples_per_s": round(rec["tested"] / dt, 1),
+                           "vs_reference": round(rec["duration_us"] / 1e6 / dt, 1),
+                           "counters_match": all(st[v] == rec[k] for k, v in KAT_FIELDS.items())}
+            del dec
+        out.append(line)
+    return out
 
 
 def cpu_baseline(code, fname, sX, sZ, p, iters, args, outs, packed):

@@ -30,6 +30,19 @@ public:
     }
 
     explicit Decoder(Quantum_LDPC_Code code) : _code(code) {}
+
+protected:
+    // int syndrome entries to the C ABI's bytes keeping the reference's two readings of an entry:
+    // its truthiness in the check update (DecoderCPU.h:178) and its exact value in the syndrome
+    // comparison (:381) -- 0 -> 0, 1 -> 1, anything else -> 2 (decodes as 1, never matches).
+    static std::vector<uint8_t> syndrome_bytes(const IntArray1d_h& s)
+    {
+        std::vector<uint8_t> out(s.size());
+        for (size_t k = 0; k < s.size(); ++k) out[k] = s[k] == 0 ? 0 : s[k] == 1 ? 1 : 2;
+        return out;
+    }
+
+public:
     virtual ~Decoder() {}
 
     virtual ErrorCode Decode(const IntArray1d_h& syndromeX, const IntArray1d_h& syndromeZ, float errorProbability,

@@ -39,7 +39,7 @@ public:
     ErrorCode Decode(const IntArray1d_h& syndromeX, const IntArray1d_h& syndromeZ, float errorProbability,
                      int maxIterations, IntArray1d_h& outErrorsX, IntArray1d_h& outErrorsZ) override
     {
-        std::vector<uint8_t> sx(syndromeX.begin(), syndromeX.end()), sz(syndromeZ.begin(), syndromeZ.end());
+        std::vector<uint8_t> sx = syndrome_bytes(syndromeX), sz = syndrome_bytes(syndromeZ);
         std::vector<uint8_t> ex(_code.n), ez(_code.n);
         uint8_t flags = 0;
         check(qec_decode_batch(dec_, sx.data(), sz.data(), 1, errorProbability, maxIterations, QEC_STOP_REF, ex.data(),

@@ -142,7 +142,8 @@ int qec_decoder_destroy(qec_decoder* dec);
  * one per part, decoded concurrently; qec_get_statistics and qec_monte_carlo shard their
  * samples the same way and sum the parts' counters (bit-identical to one device: the counters
  * do not depend on sample order).  Options apply to every part.  The _dev entry points need
- * a single-device handle: call them on qec_decoder_part(dec, k). */
+ * a single-device handle: call them on qec_decoder_part(dec, k).  Every ordinal must be >= 0
+ * (QEC_ERR_ARG otherwise: a group is GPU-only). */
 qec_decoder* qec_decoder_create_multi(const qec_code* code, const int* devices, int ndevices, size_t max_batch);
 int qec_decoder_num_parts(const qec_decoder* dec);      /* 1 for a single-device decoder */
 qec_decoder* qec_decoder_part(qec_decoder* dec, int k); /* part k (the handle itself for k = 0 of a single one) */
@@ -175,9 +176,14 @@ int qec_decoder_device(const qec_decoder* dec);         /* HIP device ordinal (o
  *     copy of the kernel whose iters[] output packs, per sector, the iterations executed in each
  *     phase instead of their count: soft | hard << 8 | agreed << 16 | jumped << 24 (soft: full
  *     arithmetic; hard: hard-message forms; agreed: the agreement path; jumped: skipped by the
- *     cycle jump; each field mod 256).  Decisions and flags are unchanged. */
+ *     cycle jump; each field mod 256).  Decisions and flags are unchanged.
+ *   QEC_OPT_TRIAGE (default 1; shipped codes, syndrome stop with N >= 2 on the Monte-Carlo
+ *     pipeline's bit-row syndromes, i.e. qec_monte_carlo): a triage kernel decides iteration 0 of
+ *     64 syndromes per wave from the syndrome patterns (triage.hip); the sectors it does not stop
+ *     are compacted into lists the decode kernel then decodes (list mode).  Bit-identical either
+ *     way; 0 decodes every sector in the decode kernel (for measurement). */
 enum { QEC_OPT_HARD_PATHS = 1, QEC_OPT_CYCLE_JUMP = 2, QEC_OPT_SCHEDULE = 3, QEC_OPT_SECTOR_SPLIT = 4,
-       QEC_OPT_PHASE_STATS = 5 };
+       QEC_OPT_PHASE_STATS = 5, QEC_OPT_TRIAGE = 6 };
 int qec_decoder_set_option(qec_decoder* dec, int option, int value);
 int qec_decoder_get_option(const qec_decoder* dec, int option, int* value);
 /* which kernel variant serves this code: writes a short name (e.g. "wave-circulant P=61 G=1") */
@@ -209,6 +215,14 @@ int qec_decode_batch_dev(qec_decoder* dec, const uint8_t* sX, const uint8_t* sZ,
 int qec_decode_batch_packed_dev(qec_decoder* dec, const uint8_t* sX, const uint8_t* sZ, size_t B,
                                 float errorProbability, int maxIterations, int stop,
                                 uint8_t* records, int32_t* iters, float* q_final, void* stream);
+/* The same with bit-row syndromes (the Monte-Carlo pipeline's layout, 72 instead of 549 bytes per
+ * P61 syndrome): sXbits [B][ceil(numEqsX / 32)] and sZbits [B][ceil(numEqsZ / 32)] 32-bit words,
+ * bit c of a row = check c (bit c % 32 of word c / 32).  Wave-circulant engine only
+ * (QEC_ERR_UNSUPPORTED otherwise).  Under the syndrome stop this is the entry point that takes
+ * the triage (QEC_OPT_TRIAGE) when no final messages are requested. */
+int qec_decode_bits_packed_dev(qec_decoder* dec, const uint32_t* sXbits, const uint32_t* sZbits, size_t B,
+                               float errorProbability, int maxIterations, int stop,
+                               uint8_t* records, int32_t* iters, float* q_final, void* stream);
 /* Host-buffer form of the packed decode (synchronous). */
 int qec_decode_batch_packed(qec_decoder* dec, const uint8_t* sX, const uint8_t* sZ, size_t B,
                             float errorProbability, int maxIterations, int stop,

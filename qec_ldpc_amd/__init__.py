@@ -26,7 +26,7 @@ CONVERGENCE_FAIL_X = 4
 CONVERGENCE_FAIL_Z = 8
 STOP = {"ref": 0, "fixed": 1, "syndrome": 2}
 ENGINE = {"auto": 0, "circulant": 1, "sparse": 2, "cpu": 3}
-OPTION = {"hard_paths": 1, "cycle_jump": 2, "schedule": 3, "sector_split": 4, "phase_stats": 5}
+OPTION = {"hard_paths": 1, "cycle_jump": 2, "schedule": 3, "sector_split": 4, "phase_stats": 5, "triage": 6}
 
 # every symbol include/qec_ldpc.h declares
 EXPORTS = (
@@ -37,6 +37,7 @@ EXPORTS = (
     "qec_decoder_num_parts", "qec_decoder_part", "qec_decoder_device", "qec_decoder_describe",
     "qec_decoder_set_option", "qec_decoder_get_option",
     "qec_decode_batch", "qec_decode_batch_dev", "qec_decode_batch_packed", "qec_decode_batch_packed_dev",
+    "qec_decode_bits_packed_dev",
     "qec_sample_fixed_weight", "qec_get_statistics",
     "qec_sample_depolarizing_dev", "qec_sample_syndrome_dev", "qec_syndrome_dev", "qec_statistics_dev",
     "qec_statistics_packed_dev", "qec_pack_decisions_dev",
@@ -123,6 +124,7 @@ def lib():
             "qec_decode_batch_dev": (i, [vp, vp, vp, sz, f, i, i, vp, vp, vp, vp, vp, vp]),
             "qec_decode_batch_packed": (i, [vp, vp, vp, sz, f, i, i, vp, vp]),
             "qec_decode_batch_packed_dev": (i, [vp, vp, vp, sz, f, i, i, vp, vp, vp, vp]),
+            "qec_decode_bits_packed_dev": (i, [vp, vp, vp, sz, f, i, i, vp, vp, vp, vp]),
             "qec_sample_fixed_weight": (i, [ctypes.c_uint32, i, sz, i, vp, vp]),
             "qec_get_statistics": (i, [vp, i, i, f, i, ctypes.c_uint32, i, ctypes.POINTER(Stats)]),
             "qec_sample_depolarizing_dev": (i, [vp, ctypes.c_uint64, ctypes.c_uint64, sz, f, vp, vp, vp]),
@@ -155,6 +157,14 @@ def _ptr(a):
     if a is None:
         return None
     return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def syndrome_bytes(s):
+    """Integer syndrome entries to the ABI's bytes, keeping both of the reference's readings of an
+    entry: its truthiness in the check update (DecoderCPU.h:178) and its exact value in the
+    syndrome comparison (:381) -- 0 -> 0, 1 -> 1, anything else -> 2 (as include/Decoder.h)."""
+    s = np.asarray(s)
+    return np.where(s == 0, 0, np.where(s == 1, 1, 2)).astype(np.uint8)
 
 
 def _u8(a, shape):
@@ -421,6 +431,22 @@ class DecoderGPU:
         _check(lib().qec_decode_batch_packed_dev(self._h, *args, ctypes.c_void_p(self._stream(stream))),
                "qec_decode_batch_packed_dev")
 
+    def decode_bits_packed_dev(self, sXbits, sZbits, p, max_iter, stop, records, iters=None, q=None, stream=None):
+        """Device-buffer decode of bit-row syndromes (int32 [B, ceil(m/32)] words, bit c of a row =
+        check c) into packed decision records [B, record_bytes()] (uint8)."""
+        import torch
+        self._single("decode_bits_packed_dev")
+        c = self.code
+        B = sXbits.shape[0]
+        args = (self._t(sXbits, "sXbits", torch.int32, (B, (c.numEqsX + 31) // 32)),
+                self._t(sZbits, "sZbits", torch.int32, (B, (c.numEqsZ + 31) // 32)),
+                B, float(p), int(max_iter), STOP[stop],
+                self._t(records, "records", torch.uint8, (B, self.record_bytes())),
+                self._t(iters, "iters", torch.int32, (B, 2), True),
+                self._t(q, "q", torch.float32, (B, (c.numEqsX + c.numEqsZ) * c.L), True))
+        _check(lib().qec_decode_bits_packed_dev(self._h, *args, ctypes.c_void_p(self._stream(stream))),
+               "qec_decode_bits_packed_dev")
+
     def sample_depolarizing_dev(self, seed, start, p, x, z, stream=None):
         """Device depolarising errors (the gap walk over Philox4x32-10 words, include/qec_ldpc.h)
         for samples [start, start + x.shape[0])."""
@@ -506,7 +532,7 @@ class DecoderGPU:
 
     def Decode(self, syndromeX, syndromeZ, errorProbability, maxIterations):
         """Decoder::Decode for one syndrome pair -> (ErrorCode, outErrorsX, outErrorsZ)."""
-        eX, eZ, flags, _, _ = self.decode_batch(np.asarray(syndromeX)[None], np.asarray(syndromeZ)[None],
+        eX, eZ, flags, _, _ = self.decode_batch(syndrome_bytes(syndromeX)[None], syndrome_bytes(syndromeZ)[None],
                                                 errorProbability, maxIterations, "ref")
         return int(flags[0]), eX[0].astype(np.int32), eZ[0].astype(np.int32)
 

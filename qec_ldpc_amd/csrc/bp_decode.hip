@@ -198,6 +198,7 @@ __device__ __forceinline__ bool hard_ok(float pp) { return pp > 0.0f && pp < 1.0
 constexpr int kMaxRL = 128;  // largest R*L a kernel argument block carries
 constexpr int kMaxTab0 = 448;  // iteration-0 table entries, (2^RX RX + 2^RZ RZ), of every instantiated variant
 constexpr int kMaxR = 16;
+constexpr uint32_t kNonBinary = 1u << 31;  // sbits: a syndrome entry of this lane is not 0 / 1 (load_sbits)
 constexpr int kMaxL = 32;
 
 struct BpArgs {
@@ -216,6 +217,10 @@ struct BpArgs {
     // sector-split launches: one word per syndrome, zeroed before the launch; each sector ORs in its
     // flags plus a done bit and the second one writes the merged flags byte (plain store)
     uint32_t* merge;
+    // list mode (MODE 2, after the triage): the syndromes whose X / Z sector goes on, and the two lengths
+    const int32_t* listX;
+    const int32_t* listZ;
+    const uint32_t* counts;
     long long B;
     int P, G, n, mX, mZ;
     int nb, recBytes;  // ceil(n / 8), 2 nb + 1
@@ -875,7 +880,7 @@ __device__ __forceinline__ bool lane_syndrome_ok(const BpArgs& a, uint32_t hdmas
         __builtin_amdgcn_sched_barrier(0);
 #endif
     }
-    return match;
+    return match && !(sbits & kNonBinary);
 }
 
 // Whether a hard sector first tries the whole-sector agreement test (var_pass_agree, the entry to
@@ -1097,7 +1102,8 @@ __device__ __forceinline__ int cycle_end(int n, int N)
     return N - 1;
 }
 
-// Syndrome bits of this lane's checks (r, i), r = 0..R-1, as bit r.
+// Syndrome bits of this lane's checks (r, i), r = 0..R-1, as bit r; kNonBinary when one of the
+// lane's syndrome bytes is neither 0 nor 1.
 template <int R, int SEC, class SH>
 __device__ __forceinline__ uint32_t load_sbits(const BpArgs& a, const Lane& ln, uint32_t b, bool in_range)
 {
@@ -1114,9 +1120,17 @@ __device__ __forceinline__ uint32_t load_sbits(const BpArgs& a, const Lane& ln, 
                 sbits |= ((w[c >> 5] >> (c & 31)) & 1u) << r;
             }
         } else {
+            // the check update takes an entry's truthiness (DecoderCPU.h:178) and the syndrome tests
+            // compare the entry exactly (:381): an entry other than 0 / 1 decodes as 1 and sets
+            // kNonBinary, which fails every syndrome test of the sector (lane_syndrome_ok)
+            uint32_t big = 0;
 #pragma unroll
-            for (int r = 0; r < R; ++r)
-                sbits |= (uint32_t)(s[(size_t)b * m + r * P + wrap(ln.i + SH::template rowoff<SEC>(a, r), P)] & 1) << r;
+            for (int r = 0; r < R; ++r) {
+                const uint32_t v = s[(size_t)b * m + r * P + wrap(ln.i + SH::template rowoff<SEC>(a, r), P)];
+                sbits |= (uint32_t)(v != 0u) << r;
+                big |= v;
+            }
+            sbits |= big > 1u ? kNonBinary : 0u;
         }
     }
     return sbits;
@@ -1310,6 +1324,7 @@ __device__ __forceinline__ void decode_sector(const BpArgs& a, Lane& ln, uint32_
             for (int l = 0; l < L; ++l) x ^= __float_as_uint(msg[r][l]);
             match &= (x != 0u) == (((sbits >> r) & 1u) != 0u);
         }
+        match &= !(sbits & kNonBinary);
         conv = true;
         syn_ok = group_all_sh<SH>(match, ln, P);
     } else {
@@ -1360,52 +1375,20 @@ __device__ __forceinline__ void decode_sector(const BpArgs& a, Lane& ln, uint32_
 template <class TU>
 constexpr int waves_per_block() { return QEC_WAVES_PER_BLOCK > 0 ? QEC_WAVES_PER_BLOCK : TU::kWavesPerBlock; }
 
+// The syndrome pair b (or, with SPLIT, its sector doX ? X : Z) of this lane's group: decode, then
+// the flags byte and iteration counts.  SPLIT: the two sectors meet in the syndrome's merge word
+// (atomicOr of flags plus a done bit; the second to arrive stores the merged byte).
 template <int RX, int RZ, int L, int STOP, class SH, class TU, bool SPLIT>
-__global__ __launch_bounds__(64 * waves_per_block<TU>(),
-                             (QEC_MIN_WAVES_PER_EU ? QEC_MIN_WAVES_PER_EU
-                                                   : STOP == QEC_STOP_SYNDROME ? TU::kMinWavesSyn : TU::kMinWaves) +
-                                 (STOP == QEC_STOP_SYNDROME ? QEC_SYN_MINW_DELTA : 0))
-void bp_decode_kernel(const BpArgs a)
+__device__ __forceinline__ void decode_group(const BpArgs& a, const float* __restrict__ tab0, uint8_t* __restrict__ stage,
+                                             int i, int gb, uint32_t b, bool in_range, bool doX)
 {
-    const int lane = threadIdx.x & 63;
-    const long long wave = (long long)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-    const int P = SH::P(a);
-    const int G = SH::kStatic ? 64 / P : a.G;
-    const int g = lane / P;
-    const int i = lane - g * P;
-    const int gb = g * P;
-    // iteration-0 tables of both sectors (iteration0), built by the workgroup before any wave leaves
-    constexpr int kTabX = (1 << RX) * RX, kTabZ = (1 << RZ) * RZ;
-    __shared__ float tab0[QEC_TABLE0 ? kTabX + kTabZ : 1];
-    if constexpr (QEC_TABLE0) {
-        const float ppt = 2.0f / 3.0f * a.errorProbability;
-        if constexpr (QEC_TABLE0_HOST && kTabX + kTabZ <= kMaxTab0) {
-            (void)ppt;
-            for (int e = threadIdx.x; e < kTabX + kTabZ; e += blockDim.x) tab0[e] = a.tab0[e];
-        } else {
-            for (int e = threadIdx.x; e < kTabX + kTabZ; e += blockDim.x)
-                tab0[e] = e < kTabX ? table0_entry<RX, L>(ppt, e) : table0_entry<RZ, L>(ppt, e - kTabX);
-        }
-        __syncthreads();
-    }
-    // this wave's decision stage for packed records (emit_decisions)
-    constexpr int kStage = stage_bytes_per_wave<L, SH>();
-    __shared__ __attribute__((aligned(8))) uint8_t stage_all[waves_per_block<TU>() * kStage];
-    uint8_t* stage = stage_all + (threadIdx.x >> 6) * kStage;
-    const long long grp = SPLIT ? wave >> 1 : wave;
-    const long long slot = grp * G + g;
-    const bool in_range = (g < G) && (slot < a.B);
-    if (!__any(in_range)) return;
-    // the syndrome index in 32 bits (launch_decode caps B below 2^31): a 64-bit index live across both
-    // sectors spilled at 96 VGPRs
-    const uint32_t b = (in_range && a.perm != nullptr) ? (uint32_t)a.perm[slot] : (uint32_t)slot;
-
+    constexpr int kTabX = (1 << RX) * RX;
     // p' = (2/3) p, as the reference writes it (DecoderCPU.h:259)
     const float pp = 2.0f / 3.0f * a.errorProbability;
+    const int P = SH::P(a);
     uint32_t flags = 0;
     int itX = 0, itZ = 0;
     Lane ln{i, gb, 4 * (gb + i), 4 * (gb + i + P), in_range};
-    const bool doX = !SPLIT || (wave & 1) == 0;  // wave-uniform
 #ifndef QEC_PREFETCH_Z
 #define QEC_PREFETCH_Z 1
 #endif
@@ -1434,6 +1417,67 @@ void bp_decode_kernel(const BpArgs a)
     }
 }
 
+// MODE 0: one wave decodes both sectors of its group of G syndromes; 1 (sector split): waves 2k and
+// 2k + 1 decode sectors X and Z of group k; 2 (list, after triage.hip): the sectors that went on
+// past the triage, listX [0, counts[0]) then listZ [0, counts[1]), G per wave, each wave looping over
+// them (the grid does not depend on the lists' device-side lengths); merged as in split mode.
+template <int RX, int RZ, int L, int STOP, class SH, class TU, int MODE>
+__global__ __launch_bounds__(64 * waves_per_block<TU>(),
+                             (QEC_MIN_WAVES_PER_EU ? QEC_MIN_WAVES_PER_EU
+                                                   : STOP == QEC_STOP_SYNDROME ? TU::kMinWavesSyn : TU::kMinWaves) +
+                                 (STOP == QEC_STOP_SYNDROME ? QEC_SYN_MINW_DELTA : 0))
+void bp_decode_kernel(const BpArgs a)
+{
+    constexpr bool SPLIT = MODE != 0;
+    const int lane = threadIdx.x & 63;
+    const long long wave = (long long)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const int P = SH::P(a);
+    const int G = SH::kStatic ? 64 / P : a.G;
+    const int g = lane / P;
+    const int i = lane - g * P;
+    const int gb = g * P;
+    // iteration-0 tables of both sectors (iteration0), built by the workgroup before any wave leaves
+    constexpr int kTabX = (1 << RX) * RX, kTabZ = (1 << RZ) * RZ;
+    __shared__ float tab0[QEC_TABLE0 ? kTabX + kTabZ : 1];
+    if constexpr (QEC_TABLE0) {
+        const float ppt = 2.0f / 3.0f * a.errorProbability;
+        if constexpr (QEC_TABLE0_HOST && kTabX + kTabZ <= kMaxTab0) {
+            (void)ppt;
+            for (int e = threadIdx.x; e < kTabX + kTabZ; e += blockDim.x) tab0[e] = a.tab0[e];
+        } else {
+            for (int e = threadIdx.x; e < kTabX + kTabZ; e += blockDim.x)
+                tab0[e] = e < kTabX ? table0_entry<RX, L>(ppt, e) : table0_entry<RZ, L>(ppt, e - kTabX);
+        }
+        __syncthreads();
+    }
+    // this wave's decision stage for packed records (emit_decisions)
+    constexpr int kStage = stage_bytes_per_wave<L, SH>();
+    __shared__ __attribute__((aligned(8))) uint8_t stage_all[waves_per_block<TU>() * kStage];
+    uint8_t* stage = stage_all + (threadIdx.x >> 6) * kStage;
+    if constexpr (MODE == 2) {
+        const long long nX = a.counts[0], nZ = a.counts[1];
+        const long long wXn = (nX + G - 1) / G, wTot = wXn + (nZ + G - 1) / G;
+        const long long nw = (long long)gridDim.x * (blockDim.x >> 6);
+        for (long long vw = wave; vw < wTot; vw += nw) {
+            const bool doX = vw < wXn;  // wave-uniform
+            const long long slot = (doX ? vw : vw - wXn) * G + g;
+            const bool in_range = (g < G) && (slot < (doX ? nX : nZ));
+            const uint32_t b = in_range ? (uint32_t)(doX ? a.listX : a.listZ)[slot] : 0u;
+            decode_group<RX, RZ, L, STOP, SH, TU, true>(a, tab0, stage, i, gb, b, in_range, doX);
+        }
+        return;
+    }
+    const long long grp = SPLIT ? wave >> 1 : wave;
+    const long long slot = grp * G + g;
+    const bool in_range = (g < G) && (slot < a.B);
+    if (!__any(in_range)) return;
+    // the syndrome index in 32 bits (launch_decode caps B below 2^31): a 64-bit index live across both
+    // sectors spilled at 96 VGPRs
+    const uint32_t b = (in_range && a.perm != nullptr) ? (uint32_t)a.perm[slot] : (uint32_t)slot;
+    const bool doX = !SPLIT || (wave & 1) == 0;  // wave-uniform
+    decode_group<RX, RZ, L, STOP, SH, TU, SPLIT>(a, tab0, stage, i, gb, b, in_range, doX);
+}
+
 // ---- variant table ----------------------------------------------------------
 using KernelFn = void (*)(const BpArgs);
 
@@ -1458,6 +1502,7 @@ using ShiftsP7 = GeneratedShifts<3, 3, 6, 7, 2, 3, TuneP7::kRelabel, TuneP7::kMa
 #endif
 KernelFn p61_minreg_kernel(int stop, bool split);  // bp_decode_p61.hip
 KernelFn p7_minreg_kernel(int stop, bool split);   // bp_decode_p61.hip
+KernelFn p7_minreg_list_kernel();                  // bp_decode_p61.hip
 
 KernelFn phase_kernel(int P, int stop);  // bp_decode_phase.hip
 
@@ -1465,25 +1510,26 @@ KernelFn phase_kernel(int P, int stop);  // bp_decode_phase.hip
 KernelFn p61_minreg_kernel(int stop, bool split)
 {
     if (stop == QEC_STOP_REF)
-        return split ? bp_decode_kernel<4, 5, 10, QEC_STOP_REF, ShiftsP61, TuneP61MinReg, true>
-                     : bp_decode_kernel<4, 5, 10, QEC_STOP_REF, ShiftsP61, TuneP61MinReg, false>;
+        return split ? bp_decode_kernel<4, 5, 10, QEC_STOP_REF, ShiftsP61, TuneP61MinReg, 1>
+                     : bp_decode_kernel<4, 5, 10, QEC_STOP_REF, ShiftsP61, TuneP61MinReg, 0>;
     if (stop == QEC_STOP_FIXED)
-        return split ? bp_decode_kernel<4, 5, 10, QEC_STOP_FIXED, ShiftsP61, TuneP61MinReg, true>
-                     : bp_decode_kernel<4, 5, 10, QEC_STOP_FIXED, ShiftsP61, TuneP61MinReg, false>;
+        return split ? bp_decode_kernel<4, 5, 10, QEC_STOP_FIXED, ShiftsP61, TuneP61MinReg, 1>
+                     : bp_decode_kernel<4, 5, 10, QEC_STOP_FIXED, ShiftsP61, TuneP61MinReg, 0>;
 #if QEC_P61_SYN_MINREG
     if (stop == QEC_STOP_SYNDROME)
-        return split ? bp_decode_kernel<4, 5, 10, QEC_STOP_SYNDROME, ShiftsP61, TuneP61MinReg, true>
-                     : bp_decode_kernel<4, 5, 10, QEC_STOP_SYNDROME, ShiftsP61, TuneP61MinReg, false>;
+        return split ? bp_decode_kernel<4, 5, 10, QEC_STOP_SYNDROME, ShiftsP61, TuneP61MinReg, 1>
+                     : bp_decode_kernel<4, 5, 10, QEC_STOP_SYNDROME, ShiftsP61, TuneP61MinReg, 0>;
 #endif
     return nullptr;
 }
 KernelFn p7_minreg_kernel(int stop, bool split)
 {
     if (stop == QEC_STOP_SYNDROME)
-        return split ? bp_decode_kernel<3, 3, 6, QEC_STOP_SYNDROME, ShiftsP7, TuneP7MinReg, true>
-                     : bp_decode_kernel<3, 3, 6, QEC_STOP_SYNDROME, ShiftsP7, TuneP7MinReg, false>;
+        return split ? bp_decode_kernel<3, 3, 6, QEC_STOP_SYNDROME, ShiftsP7, TuneP7MinReg, 1>
+                     : bp_decode_kernel<3, 3, 6, QEC_STOP_SYNDROME, ShiftsP7, TuneP7MinReg, 0>;
     return nullptr;
 }
+KernelFn p7_minreg_list_kernel() { return bp_decode_kernel<3, 3, 6, QEC_STOP_SYNDROME, ShiftsP7, TuneP7MinReg, 2>; }
 #elif defined(QEC_PHASE_TU)
 // The instrumented kernels of the shipped codes (QEC_OPT_PHASE_STATS, one wave per syndrome):
 // iters[] reports per sector soft | hard << 8 | agreed << 16 | jumped << 24 iterations.
@@ -1492,13 +1538,13 @@ struct TuneP7Phase : TuneP7 {};
 KernelFn phase_kernel(int P, int stop)
 {
     if (P == 61) {
-        if (stop == QEC_STOP_REF) return bp_decode_kernel<4, 5, 10, QEC_STOP_REF, ShiftsP61, TuneP61Phase, false>;
-        if (stop == QEC_STOP_FIXED) return bp_decode_kernel<4, 5, 10, QEC_STOP_FIXED, ShiftsP61, TuneP61Phase, false>;
-        return bp_decode_kernel<4, 5, 10, QEC_STOP_SYNDROME, ShiftsP61, TuneP61Phase, false>;
+        if (stop == QEC_STOP_REF) return bp_decode_kernel<4, 5, 10, QEC_STOP_REF, ShiftsP61, TuneP61Phase, 0>;
+        if (stop == QEC_STOP_FIXED) return bp_decode_kernel<4, 5, 10, QEC_STOP_FIXED, ShiftsP61, TuneP61Phase, 0>;
+        return bp_decode_kernel<4, 5, 10, QEC_STOP_SYNDROME, ShiftsP61, TuneP61Phase, 0>;
     }
-    if (stop == QEC_STOP_REF) return bp_decode_kernel<3, 3, 6, QEC_STOP_REF, ShiftsP7, TuneP7Phase, false>;
-    if (stop == QEC_STOP_FIXED) return bp_decode_kernel<3, 3, 6, QEC_STOP_FIXED, ShiftsP7, TuneP7Phase, false>;
-    return bp_decode_kernel<3, 3, 6, QEC_STOP_SYNDROME, ShiftsP7, TuneP7Phase, false>;
+    if (stop == QEC_STOP_REF) return bp_decode_kernel<3, 3, 6, QEC_STOP_REF, ShiftsP7, TuneP7Phase, 0>;
+    if (stop == QEC_STOP_FIXED) return bp_decode_kernel<3, 3, 6, QEC_STOP_FIXED, ShiftsP7, TuneP7Phase, 0>;
+    return bp_decode_kernel<3, 3, 6, QEC_STOP_SYNDROME, ShiftsP7, TuneP7Phase, 0>;
 }
 #else
 
@@ -1513,6 +1559,8 @@ struct Variant {
     KernelFn phase[3];  // QEC_OPT_PHASE_STATS: instrumented kernels (shipped codes only)
     int (*fill_tab0)(float pp, float* out);  // host iteration-0 tables (QEC_TABLE0_HOST)
     const char* name;
+    KernelFn list = nullptr;  // syndrome stop, list mode (MODE 2: the sectors the triage passed on)
+    int min_waves_syn = 1;    // its occupancy (waves per SIMD), for the list launch's grid
 };
 
 // Both sectors' iteration-0 tables on the host, entry for entry what the device's table0_entry
@@ -1532,18 +1580,20 @@ template <int J, int K, int L, class SH, class TU, bool WITH_SPLIT>
 static Variant make_variant(int P, int S, int T, const char* name)
 {
     Variant v{J, K, L, P, S, T, TU::kRelabel, TU::kSplit && WITH_SPLIT, waves_per_block<TU>(),
-              {bp_decode_kernel<J, K, L, QEC_STOP_REF, SH, TU, false>,
-               bp_decode_kernel<J, K, L, QEC_STOP_FIXED, SH, TU, false>,
-               bp_decode_kernel<J, K, L, QEC_STOP_SYNDROME, SH, TU, false>},
+              {bp_decode_kernel<J, K, L, QEC_STOP_REF, SH, TU, 0>,
+               bp_decode_kernel<J, K, L, QEC_STOP_FIXED, SH, TU, 0>,
+               bp_decode_kernel<J, K, L, QEC_STOP_SYNDROME, SH, TU, 0>},
               {nullptr, nullptr, nullptr},
               {nullptr, nullptr, nullptr},
               fill_tab0<J, K, L>,
               name};
     if constexpr (WITH_SPLIT) {
-        v.split[QEC_STOP_REF] = bp_decode_kernel<J, K, L, QEC_STOP_REF, SH, TU, true>;
-        v.split[QEC_STOP_FIXED] = bp_decode_kernel<J, K, L, QEC_STOP_FIXED, SH, TU, true>;
-        v.split[QEC_STOP_SYNDROME] = bp_decode_kernel<J, K, L, QEC_STOP_SYNDROME, SH, TU, true>;
+        v.split[QEC_STOP_REF] = bp_decode_kernel<J, K, L, QEC_STOP_REF, SH, TU, 1>;
+        v.split[QEC_STOP_FIXED] = bp_decode_kernel<J, K, L, QEC_STOP_FIXED, SH, TU, 1>;
+        v.split[QEC_STOP_SYNDROME] = bp_decode_kernel<J, K, L, QEC_STOP_SYNDROME, SH, TU, 1>;
+        v.list = bp_decode_kernel<J, K, L, QEC_STOP_SYNDROME, SH, TU, 2>;
     }
+    v.min_waves_syn = TU::kMinWavesSyn;
     return v;
 }
 // Tune<min waves per SIMD, relabel, zero-skip, short division, hard-message paths, sector split,
@@ -1599,6 +1649,7 @@ static Variant gen_p7()
     if (QEC_P61_MINREG) {
         v.fn[QEC_STOP_SYNDROME] = p7_minreg_kernel(QEC_STOP_SYNDROME, false);
         v.split[QEC_STOP_SYNDROME] = p7_minreg_kernel(QEC_STOP_SYNDROME, true);
+        v.list = p7_minreg_list_kernel();
     }
     return v;
 }
@@ -1708,6 +1759,75 @@ int launch_decode(const void* variant, const Code& c, const uint8_t* sX, const u
                        dim3(64 * wavesPerBlock), 0, stream, a);
     hipError_t err = hipGetLastError();
     if (err != hipSuccess) return fail(QEC_ERR_HIP, std::string("bp_decode launch: ") + hipGetErrorString(err));
+    return QEC_OK;
+}
+
+bool decode_has_list(const void* variant) { return static_cast<const Variant*>(variant)->list != nullptr; }
+
+// The iteration-0 pattern masks of both sectors (triage.hip): bit idx of hd = pattern idx decides 1
+// (some table entry >= 0.5f), of cv = its R messages all lie outside (0.01, 0.99) -- the host table's
+// entries under pattern_masks' compares.  pats = {hdX, cvX, hdZ, cvZ}; false if they do not fit.
+bool decode_pattern_masks(const void* variant, float errorProbability, uint32_t pats[4])
+{
+    const Variant* v = static_cast<const Variant*>(variant);
+    if (v->J > 5 || v->K > 5) return false;
+    float tab[kMaxTab0];
+    if (!v->fill_tab0(2.0f / 3.0f * errorProbability, tab)) return false;
+    const float* t = tab;
+    for (int sec = 0; sec < 2; ++sec) {
+        const int R = sec ? v->K : v->J;
+        uint32_t hd = 0, cv = 0;
+        for (int idx = 0; idx < (1 << R); ++idx) {
+            bool h = false, c = true;
+            for (int r = 0; r < R; ++r) {
+                h |= t[idx * R + r] >= 0.5f;
+                c &= !(t[idx * R + r] > 0.01f && t[idx * R + r] < 0.99f);
+            }
+            hd |= (uint32_t)h << idx;
+            cv |= (uint32_t)c << idx;
+        }
+        pats[2 * sec] = hd;
+        pats[2 * sec + 1] = cv;
+        t += (1 << R) * R;
+    }
+    return true;
+}
+
+// List-mode decode (syndrome stop, bit-row syndromes, packed records) of the sectors triage.hip
+// passed on: listX [0, counts[0]), listZ [0, counts[1]) on the device; at most 2 B sectors.  A
+// grid of about one wave per resident slot loops over them.
+int launch_decode_list(const void* variant, const Code& c, const uint8_t* sX, const uint8_t* sZ, long long B,
+                       float errorProbability, int maxIter, int hardPaths, uint8_t* rec, int32_t* iters,
+                       uint32_t* merge, const int32_t* listX, const int32_t* listZ, const uint32_t* counts,
+                       hipStream_t stream)
+{
+    const Variant* v = static_cast<const Variant*>(variant);
+    if (!v->list) return fail(QEC_ERR_UNSUPPORTED, "bp_decode: no list-mode kernel for this code");
+    if (B <= 0) return QEC_OK;
+    if (B >= (1LL << 31)) return fail(QEC_ERR_ARG, "bp_decode: at most 2^31 - 1 syndromes per launch");
+    BpArgs a{};
+    a.sX = sX; a.sZ = sZ; a.sbits = 1;
+    a.wX = (c.mX + 31) / 32; a.wZ = (c.mZ + 31) / 32;
+    a.rec = rec; a.iters = iters; a.merge = merge;
+    a.listX = listX; a.listZ = listZ; a.counts = counts;
+    a.B = B; a.P = c.P; a.G = 64 / c.P;
+    a.n = c.n; a.mX = c.mX; a.mZ = c.mZ;
+    a.nb = (c.n + 7) / 8; a.recBytes = 2 * a.nb + 1;
+    a.errorProbability = errorProbability;
+    a.maxIter = maxIter < 0 ? 0 : maxIter;
+    a.stop = QEC_STOP_SYNDROME;
+    a.hardPaths = hardPaths & (QEC_HP_FORMS | QEC_HP_CYCLE);
+    if (QEC_TABLE0_HOST) v->fill_tab0(2.0f / 3.0f * errorProbability, a.tab0);
+    relabel(c.EX.data(), c.J, c.L, c.P, v->relabel, a.SX, a.DX, a.CX);
+    relabel(c.EZ.data(), c.K, c.L, c.P, v->relabel, a.SZ, a.DZ, a.CZ);
+    const long long need = (2 * B + a.G - 1) / a.G;  // waves for every sector
+    const long long cap = 1024LL * v->min_waves_syn;  // one per resident slot of the chip
+    const long long waves = need < cap ? need : cap;
+    const int wpb = v->waves_per_block;
+    const long long blocks = (waves + wpb - 1) / wpb;
+    hipLaunchKernelGGL(v->list, dim3((unsigned)blocks), dim3(64 * wpb), 0, stream, a);
+    hipError_t err = hipGetLastError();
+    if (err != hipSuccess) return fail(QEC_ERR_HIP, std::string("bp_decode list launch: ") + hipGetErrorString(err));
     return QEC_OK;
 }
 

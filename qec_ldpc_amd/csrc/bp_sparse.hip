@@ -148,7 +148,9 @@ __global__ __launch_bounds__(kSparseThreads) void bp_sparse_kernel(const SparseA
 
     for (long long b = blockIdx.x; b < a.B; b += gridDim.x) {
         // syndromes in, InitVarNodes: every edge starts at p' (DecoderCPU.h:135-148, 265-267)
-        for (int c = tid; c < m; c += nt) syn[c] = (c < mX ? a.sX[b * mX + c] : a.sZ[b * mZ + (c - mX)]) & 1;
+        // the entry as given: the check update takes its truthiness, the syndrome tests compare it
+        // exactly (DecoderCPU.h:178, :381), so an entry other than 0/1 never matches a parity
+        for (int c = tid; c < m; c += nt) syn[c] = c < mX ? a.sX[b * mX + c] : a.sZ[b * mZ + (c - mX)];
         for (int e = tid; e < E; e += nt) msg[e] = pp;
         __syncthreads();
 

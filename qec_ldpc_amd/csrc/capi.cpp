@@ -24,6 +24,16 @@ long long schedule_max_batch();
 int launch_schedule(const uint8_t* sX, const uint8_t* sZ, bool sbits, long long B, int mX, int mZ, void* ws,
                     uint32_t* zero_merge, int32_t** perm_out, hipStream_t st);
 bool decode_uses_split(const void* variant, int stop, int split, long long B);
+bool decode_has_list(const void* variant);
+bool decode_pattern_masks(const void* variant, float errorProbability, uint32_t pats[4]);
+int launch_decode_list(const void* variant, const Code& c, const uint8_t* sX, const uint8_t* sZ, long long B,
+                       float errorProbability, int maxIter, int hardPaths, uint8_t* rec, int32_t* iters,
+                       uint32_t* merge, const int32_t* listX, const int32_t* listZ, const uint32_t* counts,
+                       hipStream_t stream);
+bool triage_supported(const Code& c);
+int launch_triage(const Code& c, const uint32_t* sX, const uint32_t* sZ, long long B, const uint32_t pats[4],
+                  uint8_t* rec, int32_t* iters, uint32_t* merge, int32_t* listX, int32_t* listZ, uint32_t* counts,
+                  hipStream_t st);
 bool decode_has_phase_stats(const void* variant, int stop);
 int launch_sample_depolarizing(uint64_t seed, uint64_t start, long long B, int n, float p, uint8_t* x, uint8_t* z,
                                hipStream_t st);
@@ -71,11 +81,13 @@ struct qec_decoder {
     int schedule = 1;               // QEC_OPT_SCHEDULE (0 off, 1 auto, 2 always)
     int sector_split = 1;           // QEC_OPT_SECTOR_SPLIT (0 off, 1 auto, 2 on)
     int phase_stats = 0;            // QEC_OPT_PHASE_STATS
+    int triage = 1;                 // QEC_OPT_TRIAGE
     // workspace shared by every launch of this handle (dispatch order, split-flag merge words,
     // sparse byte staging for packed output); ws_ev marks the last launch that used it, so a call
     // on another stream waits for it (stream-ordered reuse)
     DeviceArray<uint8_t> sched;
     DeviceArray<uint32_t> merge;
+    DeviceArray<int32_t> tlist;  // triage: listX [B], listZ [B], counts [2]
     hipEvent_t ws_ev = nullptr;
     hipStream_t ws_stream = nullptr;
     bool ws_used = false;
@@ -97,6 +109,8 @@ struct qec_decoder {
         for (qec_decoder* p : parts) delete p;
         if (cpu) cpu_plan_free(cpu);
         if (parts.empty() && !cpu) {
+            // the member device arrays are freed after this body, on this device too;
+            // qec_decoder_destroy restores the caller's device afterwards
             (void)hipSetDevice(device);
             if (ws_ev) (void)hipEventDestroy(ws_ev);
             if (stream) (void)hipStreamDestroy(stream);
@@ -352,6 +366,14 @@ qec_decoder* qec_decoder_create_engine(const qec_code* h, int device, size_t max
 qec_decoder* qec_decoder_create_multi(const qec_code* h, const int* devices, int ndevices, size_t max_batch)
 {
     if (!h || !devices || ndevices <= 0) { fail(QEC_ERR_ARG, "qec_decoder_create_multi: bad argument"); return nullptr; }
+    for (int k = 0; k < ndevices; ++k)
+        if (devices[k] < 0) {
+            // a CPU-engine part would decode host batches but fail the device-side entry points
+            // (statistics, Monte-Carlo) of the group: groups are GPU-only
+            fail(QEC_ERR_ARG, "qec_decoder_create_multi: device ordinals must be >= 0 (the CPU engine is device -1 of "
+                              "qec_decoder_create)");
+            return nullptr;
+        }
     std::unique_ptr<qec_decoder> g(new (std::nothrow) qec_decoder);
     if (!g) { fail(QEC_ERR_NOMEM, "qec_decoder_create_multi: out of memory"); return nullptr; }
     for (int k = 0; k < ndevices; ++k) {
@@ -392,7 +414,12 @@ int qec_decoder_device(const qec_decoder* d)
 
 int qec_decoder_destroy(qec_decoder* d)
 {
+    // every part's streams, events and device arrays are freed on its own device; the caller's
+    // current device is restored afterwards (as every other entry point does)
+    int prev = -1;
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
     delete d;
+    if (prev >= 0) (void)hipSetDevice(prev);
     return QEC_OK;
 }
 
@@ -426,6 +453,7 @@ int qec_decoder_set_option(qec_decoder* d, int option, int value)
             return fail(QEC_ERR_UNSUPPORTED, "qec_decoder_set_option: QEC_OPT_PHASE_STATS needs a shipped code's kernels");
         d->phase_stats = value != 0;
         return QEC_OK;
+    case QEC_OPT_TRIAGE: d->triage = value != 0; return QEC_OK;
     default: return fail(QEC_ERR_ARG, "qec_decoder_set_option: unknown option");
     }
 }
@@ -439,6 +467,7 @@ int qec_decoder_get_option(const qec_decoder* d, int option, int* value)
     case QEC_OPT_SCHEDULE: *value = d->schedule; return QEC_OK;
     case QEC_OPT_SECTOR_SPLIT: *value = d->sector_split; return QEC_OK;
     case QEC_OPT_PHASE_STATS: *value = d->phase_stats; return QEC_OK;
+    case QEC_OPT_TRIAGE: *value = d->triage; return QEC_OK;
     default: return fail(QEC_ERR_ARG, "qec_decoder_get_option: unknown option");
     }
 }
@@ -489,6 +518,25 @@ int dispatch_decode(qec_decoder* d, const uint8_t* sX, const uint8_t* sZ, long l
     }
     const int hp = (d->hard_paths ? (QEC_HP_FORMS | (d->cycle_jump ? QEC_HP_CYCLE : 0)) : 0) |
                    (d->phase_stats ? QEC_HP_PHASE : 0);
+    // syndrome stop on bit rows into records (the Monte-Carlo pipeline): triage iteration 0 for 64
+    // syndromes per wave, then decode only the sectors it passes on (triage.hip, list mode)
+    uint32_t pats[4];
+    if (d->triage && !d->phase_stats && stop == QEC_STOP_SYNDROME && sbits && rec != nullptr && q == nullptr &&
+        maxIter >= 2 && B < (1LL << 31) && decode_has_list(d->variant) && triage_supported(c) &&
+        decode_pattern_masks(d->variant, p, pats)) {
+        if ((rc = ws_reserve(d->merge, (size_t)B, st, "decode")) || (rc = ws_reserve(d->tlist, 2 * (size_t)B + 2, st, "decode")))
+            return rc;
+        int32_t* lX = d->tlist.data();
+        int32_t* lZ = lX + B;
+        uint32_t* cnt = reinterpret_cast<uint32_t*>(lZ + B);
+        QEC_HIP_CHECK(hipMemsetAsync(cnt, 0, 2 * sizeof(uint32_t), st));
+        rc = launch_triage(c, reinterpret_cast<const uint32_t*>(sX), reinterpret_cast<const uint32_t*>(sZ), B, pats, rec,
+                           iters, d->merge.data(), lX, lZ, cnt, st);
+        if (!rc)
+            rc = launch_decode_list(d->variant, c, sX, sZ, B, p, maxIter, hp, rec, iters, d->merge.data(), lX, lZ, cnt, st);
+        if (rc) return rc;
+        return ws_release(d, st);
+    }
     const bool split = !d->phase_stats && decode_uses_split(d->variant, stop, d->sector_split, B);
     if (split && (rc = ws_reserve(d->merge, (size_t)B, st, "decode"))) return rc;
     const int32_t* perm = nullptr;
@@ -634,6 +682,20 @@ int qec_decode_batch_packed_dev(qec_decoder* d, const uint8_t* sX, const uint8_t
     QEC_DEVICE_SCOPE(d->device);
     return dispatch_decode(d, sX, sZ, (long long)B, p, maxIter, stop, nullptr, nullptr, nullptr, records, iters, q,
                            static_cast<hipStream_t>(stream));
+}
+
+int qec_decode_bits_packed_dev(qec_decoder* d, const uint32_t* sX, const uint32_t* sZ, size_t B, float p, int maxIter,
+                               int stop, uint8_t* records, int32_t* iters, float* q, void* stream)
+{
+    int rc = check_decode_args(d, sX, sZ, B, stop);
+    if (rc || (rc = single_device_only(d, "qec_decode_bits_packed_dev"))) return rc;
+    if (B && !records) return fail(QEC_ERR_ARG, "decode: null record buffer");
+    if (d->engine == QEC_ENGINE_SPARSE)
+        return fail(QEC_ERR_UNSUPPORTED, "qec_decode_bits_packed_dev: bit-row syndromes need the wave-circulant engine");
+    QEC_DEVICE_SCOPE(d->device);
+    return dispatch_decode(d, reinterpret_cast<const uint8_t*>(sX), reinterpret_cast<const uint8_t*>(sZ), (long long)B, p,
+                           maxIter, stop, nullptr, nullptr, nullptr, records, iters, q, static_cast<hipStream_t>(stream),
+                           true);
 }
 
 int qec_decode_batch(qec_decoder* d, const uint8_t* sX, const uint8_t* sZ, size_t B, float p, int maxIter, int stop,

@@ -94,7 +94,7 @@ int decode_sector(const CpuSector& S, int n, const uint8_t* syn, float errorProb
         for (int c = 0; c < m; ++c) {
             uint32_t x = 0;
             for (int k = 0; k < dc; ++k) x ^= e[S.chk_var[(size_t)c * dc + k]];
-            if ((x & 1u) != (syn[c] & 1u)) return false;
+            if ((x & 1u) != syn[c]) return false;  // exact compare (:381): an entry other than 0/1 never matches
         }
         return true;
     };
@@ -107,7 +107,7 @@ int decode_sector(const CpuSector& S, int n, const uint8_t* syn, float errorProb
         for (int c = 0; c < m; ++c) {
             const float* qc = q + (size_t)c * dc;
             float* rc = r + (size_t)c * dc;
-            const bool s = syn[c] & 1u;
+            const bool s = syn[c] != 0;  // truthiness (:178)
             for (int i = 0; i < dc; ++i) {
                 float t = 1.0f;
                 for (int k = 0; k < dc; ++k)

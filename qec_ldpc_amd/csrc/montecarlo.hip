@@ -657,6 +657,158 @@ __global__ __launch_bounds__(64 * kStatBlockWaves) void statistics_packed_kernel
     stat_flush(part, c, iters != nullptr ? C_N + 2 : C_N, counters);
 }
 
+// The same counters with one lane per sample (statistics_rows_kernel).  A wave takes S consecutive
+// samples: their packed-error rows and decision records are two contiguous byte ranges, copied into
+// the wave's LDS with 16-byte loads (the kernel above loads one byte per lane: 64 B per wave
+// instruction, latency-bound at ~1.4 TB/s).  Lane s then reads sample s's rows as dwords (byte
+// alignment by funnel shift), ORs its x, z and residual bytes, and the wave adds its samples' 0/1
+// outcomes with ballot popcounts (scalar).  The rare sample needing the I-P columns (no syndrome
+// failure, nonzero residual) has its residual words formed by the wave in LDS and goes through
+// logical_from_columns, one at a time.
+constexpr int kRowWaves = 2;          // waves per workgroup
+constexpr int kRowLdsPerWave = 20608;  // bytes: S (estride + recB) + 2 x 16 of alignment slack, S <= 64 (P61: 19 904)
+
+// bytes [src, src + nb) of global memory into LDS at dst + (src & 15): 16-byte loads over the
+// aligned body, single bytes for the unaligned head and tail (nothing outside the range is read)
+__device__ __forceinline__ void stage_range(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src, int nb, int lane)
+{
+    const uintptr_t s0 = reinterpret_cast<uintptr_t>(src), s1 = s0 + (uintptr_t)nb;
+    const uintptr_t a0 = s0 & ~(uintptr_t)15;
+    uintptr_t b0 = (s0 + 15) & ~(uintptr_t)15, b1 = s1 & ~(uintptr_t)15;
+    if (b0 > b1) b0 = b1 = s1;  // the whole range lies inside one 16-byte line: bytes only
+    const int head = (int)(b0 - s0), tail = (int)(s1 - b1);
+    if (lane < head) dst[(s0 - a0) + lane] = src[lane];
+    if (lane < tail) dst[(b1 - a0) + lane] = *reinterpret_cast<const uint8_t*>(b1 + lane);
+    const int nv = (int)((b1 - b0) >> 4);
+    const uint4* __restrict__ g = reinterpret_cast<const uint4*>(b0);
+    uint4* __restrict__ l = reinterpret_cast<uint4*>(dst + (b0 - a0));
+    int t = lane;
+    for (; t + 192 < nv; t += 256) {  // four 16-byte loads in flight per lane
+        const uint4 v0 = g[t], v1 = g[t + 64], v2 = g[t + 128], v3 = g[t + 192];
+        l[t] = v0; l[t + 64] = v1; l[t + 128] = v2; l[t + 192] = v3;
+    }
+    for (; t < nv; t += 64) l[t] = g[t];
+}
+
+// dword k (bytes 4k .. 4k + 3) of a row starting at any byte offset o of the stage
+__device__ __forceinline__ uint32_t row_word(const uint8_t* __restrict__ stage, int o, int k)
+{
+    const int a = o + 4 * k, w = a & ~3, sh = a & 3;
+    const uint32_t lo = *reinterpret_cast<const uint32_t*>(stage + w);
+    if (sh == 0) return lo;
+    const uint32_t hi = *reinterpret_cast<const uint32_t*>(stage + w + 4);
+    return __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)sh);
+}
+
+__global__ __launch_bounds__(64 * kRowWaves) void statistics_rows_kernel(
+    const uint8_t* __restrict__ errp, int estride, const uint8_t* __restrict__ rec, const int32_t* __restrict__ iters,
+    long long B, int n, int nb, int S, const uint64_t* __restrict__ imp_cols, int imp_cw,
+    unsigned long long* __restrict__ counters)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t row_smem[];
+    __shared__ unsigned long long part[kRowWaves][C_N + 2];
+    __shared__ unsigned long long sres[kRowWaves][kMaxRecWords];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int recB = 2 * nb + 1, eb = 2 * nb;
+    const int ewords = (eb + 3) / 4;  // dwords covering a row's decision bytes
+    uint8_t* __restrict__ est = row_smem + (size_t)wv * kRowLdsPerWave;
+    uint8_t* __restrict__ rst = est + ((S * estride + 16 + 15) & ~15);
+    unsigned long long c[C_N] = {};
+    unsigned long long itx = 0, itz = 0;  // this lane's iteration sums
+    const long long step = (long long)gridDim.x * kRowWaves * S;
+    for (long long b0 = ((long long)blockIdx.x * kRowWaves + wv) * S; b0 < B; b0 += step) {
+        const int ns = (int)(B - b0 < S ? B - b0 : S);
+        const uint8_t* ge = errp + b0 * estride;
+        const uint8_t* gr = rec + b0 * recB;
+        stage_range(est, ge, ns * estride, lane);
+        stage_range(rst, gr, ns * recB, lane);
+        const bool valid = lane < ns;
+        if (iters != nullptr && valid) {
+            itx += (unsigned)iters[2 * (b0 + lane)];
+            itz += (unsigned)iters[2 * (b0 + lane) + 1];
+        }
+        wave_sync();
+        const int oe = (int)(reinterpret_cast<uintptr_t>(ge) & 15) + lane * estride;
+        const int orr = (int)(reinterpret_cast<uintptr_t>(gr) & 15) + lane * recB;
+        uint32_t ax = 0, az = 0, ar = 0;
+        if (valid) {
+            for (int k = 0; k < ewords; ++k) {
+                // byte masks of this word: x bytes [0, nb), z bytes [nb, 2 nb) (wave-uniform)
+                const int bx = nb - 4 * k, bz = eb - 4 * k;
+                const uint32_t mx = bx >= 4 ? ~0u : bx <= 0 ? 0u : (1u << (8 * bx)) - 1u;
+                const uint32_t mall = bz >= 4 ? ~0u : bz <= 0 ? 0u : (1u << (8 * bz)) - 1u;
+                const uint32_t e = row_word(est, oe, k), r = row_word(rst, orr, k);
+                ax |= e & mx;
+                az |= e & mall & ~mx;
+                ar |= (e ^ r) & mall;
+            }
+        }
+        const uint32_t f = valid ? rst[orr + eb] : 0u;
+        const bool dEX = (f & QEC_SYNDROME_FAIL_X) != 0, dEZ = (f & QEC_SYNDROME_FAIL_Z) != 0;
+        // samples needing the I-P columns: no syndrome failure, nonzero residual (the decoder found
+        // something else than the error)
+        unsigned long long need = __ballot(valid && !(dEX || dEZ) && ar != 0u);
+        unsigned long long logical = 0;
+        if (imp_cw > 0) {
+            const int nw = (eb + 7) / 8;  // 64-bit residual words (record layout)
+            while (need) {
+                const int s = __builtin_ctzll(need);
+                need &= need - 1;
+                const int oe_s = (int)(reinterpret_cast<uintptr_t>(ge) & 15) + s * estride;
+                const int or_s = (int)(reinterpret_cast<uintptr_t>(gr) & 15) + s * recB;
+                if (lane < nw) {
+                    uint64_t w = 0;
+                    for (int j = 0; j < 8; ++j) {
+                        const int t = 8 * lane + j;
+                        const uint64_t by = t < eb ? (uint64_t)(est[oe_s + t] ^ rst[or_s + t]) : 0ull;
+                        w |= by << (8 * j);
+                    }
+                    sres[wv][lane] = w;
+                }
+                wave_sync();
+                if (logical_from_columns<true>(sres[wv], nw, n, nb, imp_cols, imp_cw, lane)) logical |= 1ull << s;
+                wave_sync();
+            }
+        }
+        const unsigned long long vm = __ballot(valid), sx = __ballot(dEX), sz = __ballot(dEZ);
+        const unsigned long long ok = vm & ~(sx | sz);
+        c[C_WITHX] += __popcll(__ballot(ax != 0u));
+        c[C_WITHZ] += __popcll(__ballot(az != 0u));
+        c[C_SYNX] += __popcll(sx);
+        c[C_SYNZ] += __popcll(sz);
+        c[C_LOGICAL] += __popcll(ok & logical);
+        c[C_CORRECTED] += __popcll(ok & ~logical);
+        c[C_CONVX] += __popcll(__ballot((f & QEC_CONVERGENCE_FAIL_X) != 0));
+        c[C_CONVZ] += __popcll(__ballot((f & QEC_CONVERGENCE_FAIL_Z) != 0));
+        wave_sync();  // the stage is reused by the next chunk
+    }
+    // iteration sums: wave reduction of the per-lane values
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        itx += __shfl_xor(itx, o);
+        itz += __shfl_xor(itz, o);
+    }
+    unsigned long long cc[C_N + 2];
+#pragma unroll
+    for (int k = 0; k < C_N; ++k) cc[k] = c[k];
+    cc[C_N] = itx;
+    cc[C_N + 1] = itz;
+    // stat_flush with kRowWaves waves
+    if (lane < C_N + 2) {
+        unsigned long long v = 0;
+#pragma unroll
+        for (int k = 0; k < C_N + 2; ++k) v = lane == k ? cc[k] : v;
+        part[wv][lane] = v;
+    }
+    __syncthreads();
+    const int nc = iters != nullptr ? C_N + 2 : C_N;
+    if (threadIdx.x < nc) {
+        unsigned long long v = 0;
+        for (int w = 0; w < kRowWaves; ++w) v += part[w][threadIdx.x];
+        if (v) atomicAdd(&counters[threadIdx.x], v);
+    }
+}
+
 // ---- launchers --------------------------------------------------------------
 static int launch_check(const char* what)
 {
@@ -718,13 +870,17 @@ static int launch_mc_gap(const McArgsHost& h, hipStream_t st)
     a.wZ = (c.mZ + 31) / 32;
     a.w32 = a.ew + a.wX + a.wZ;
     a.estride = h.errp_words ? 4 * a.ew : 2 * a.nb;
-    // at most 16 KiB of sample state per wave
-    a.spw = std::max(1, std::min(gap_spw(h.B), 16384 / (4 * a.w32)));
+    // sample state per wave: what the 64 KiB LDS stage holds beside the gap table T (n + 1 words) and
+    // the exponent table E, split over the workgroup's waves (at most gap_spw's choice)
+    const int ne = a.varEdge ? 0 : (c.J + c.K) * c.L;
+    const long long free_words = 16384LL - ((long long)c.n + 1 + ne);
+    const long long spw_fit = free_words > 0 ? free_words / ((long long)kGapWaves * a.w32) : 0;
+    if (spw_fit < 1) return fail(QEC_ERR_UNSUPPORTED, "mc front end: code too long for the LDS stage");
+    a.spw = (int)std::min<long long>(gap_spw(h.B), spw_fit);
     if ((long long)a.spw * std::max<long long>({(long long)c.mX, (long long)c.mZ, 2LL * a.nb}) >= 65536)
         return fail(QEC_ERR_UNSUPPORTED, "mc front end: code too long");
     a.magicX = magic_of(c.mX); a.magicZ = magic_of(c.mZ); a.magicE = magic_of(2 * a.nb);
     a.magicWX = magic_of(a.wX); a.magicWZ = magic_of(a.wZ); a.magicEW = magic_of(a.ew);
-    const int ne = a.varEdge ? 0 : (c.J + c.K) * c.L;
     const size_t smem = 4 * ((size_t)c.n + 1 + ne + (size_t)kGapWaves * a.spw * a.w32);
     if (smem > 64 * 1024) return fail(QEC_ERR_UNSUPPORTED, "mc front end: code too long for the LDS stage");
     const long long per_block = (long long)kGapWaves * a.spw;
@@ -783,6 +939,19 @@ int launch_statistics_packed(const Code& c, const uint64_t* imp_cols, const uint
     const int nb = (c.n + 7) / 8;
     if ((2 * nb + 7) / 8 > kMaxRecWords || c.imp_col_words > 64)
         return fail(QEC_ERR_UNSUPPORTED, "packed statistics kernel: code too long");
+    static const int rows = [] { const char* e = std::getenv("QEC_STAT_ROWS"); return e ? std::atoi(e) : 1; }();
+    if (rows) {
+        int S = 64;
+        while (S >= 16 && S * (estride + 2 * nb + 1) + 64 > kRowLdsPerWave) S /= 2;
+        if (S >= 16) {
+            static const int maxb = [] { const char* e = std::getenv("QEC_STAT_BLOCKS"); const int v = e ? std::atoi(e) : 0; return v > 0 ? v : 1024; }();
+            const long long blocks = std::min<long long>((B + kRowWaves * S - 1) / (kRowWaves * S), maxb);
+            hipLaunchKernelGGL(statistics_rows_kernel, dim3((unsigned)blocks), dim3(64 * kRowWaves),
+                               (size_t)kRowWaves * kRowLdsPerWave, st, errp, estride, rec, iters, B, c.n, nb, S, imp_cols,
+                               c.imp_col_words, counters);
+            return launch_check("statistics_rows");
+        }
+    }
     const int nj = (8 * ((2 * nb + 7) / 8) + 63) / 64;
     constexpr int U = QEC_STAT_U;
     static const int maxb = [] { const char* e = std::getenv("QEC_STAT_BLOCKS"); const int v = e ? std::atoi(e) : 0; return v > 0 ? v : kStatMaxBlocks; }();

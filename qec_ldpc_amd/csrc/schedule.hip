@@ -45,6 +45,12 @@ constexpr int kHistSplitLong = QEC_HIST_SPLIT;
 constexpr int kShortRows = 128;  // mX + mZ up to this many bytes: one thread per syndrome
 constexpr int kMaxChunks = 1024;
 constexpr int kMaxChunk = 4096;
+#ifndef QEC_SCHED_FUSED_MAX
+#define QEC_SCHED_FUSED_MAX 128  // experiments: 0 always takes the separate offsets pass
+#endif
+#ifndef QEC_SCHED_TARGET_CHUNKS
+#define QEC_SCHED_TARGET_CHUNKS 128  // chunks (histogram workgroups) aimed for when the batch is small
+#endif
 
 // Weight (bit 0 of each byte) of bytes [g0, g1) of s, read by one thread with 16-byte loads at
 // aligned addresses; bytes outside the range are masked off (the first and last loads may
@@ -92,7 +98,7 @@ __global__ __launch_bounds__(kHistThreads) void schedule_hist_kernel(const uint8
     const long long r1 = r0 + chunk < B ? r0 + chunk : B;
     if (t < kBuckets) h[t] = 0;
     __syncthreads();
-    for (long long b = r0 + t / SPLIT; b - (t / SPLIT) < r1; b += kHistThreads / SPLIT) {
+    for (long long b = r0 + t / SPLIT; b - (t / SPLIT) < r1; b += blockDim.x / SPLIT) {
         uint32_t w = 0;
         if (b < r1) {
             const long long x0 = b * mX + (long long)(mX * q / SPLIT), x1 = b * mX + (long long)(mX * (q + 1) / SPLIT);
@@ -127,7 +133,7 @@ __global__ __launch_bounds__(kHistThreads) void schedule_hist_bits_kernel(const 
     const long long r1 = r0 + chunk < B ? r0 + chunk : B;
     if (t < kBuckets) h[t] = 0;
     __syncthreads();
-    for (long long b = r0 + t; b < r1; b += kHistThreads) {
+    for (long long b = r0 + t; b < r1; b += blockDim.x) {
         uint32_t w = 0;
         for (int k = 0; k < wX; ++k) w += __popc(sX[b * wX + k]);
         for (int k = 0; k < wZ; ++k) w += __popc(sZ[b * wZ + k]);
@@ -190,12 +196,65 @@ __global__ __launch_bounds__(kScatThreads) void schedule_scatter_kernel(const ui
     for (long long b = r0 + t; b < r1; b += kScatThreads) perm[atomicAdd(&cur[key[b]], 1u)] = (int32_t)b;
 }
 
+// Offsets and scatter in one launch, for at most kMaxFusedChunks chunks: workgroup c reads the whole
+// [chunks][256] count matrix (at most 128 KiB, L2-resident after the histogram wrote it), forms the
+// bucket totals and its own chunk prefixes in LDS, and scatters as schedule_scatter_kernel.  One
+// dependent launch fewer for the batches where the order pass is mostly launch latency (P7 65 536:
+// three passes 46 us, of which the 16-workgroup histogram 36 us, profiles/r03/).
+constexpr int kMaxFusedChunks = QEC_SCHED_FUSED_MAX;
+__global__ __launch_bounds__(kScatThreads) void schedule_scatter_fused_kernel(const uint8_t* __restrict__ key, long long B,
+                                                                            int chunk, int nch,
+                                                                            const uint32_t* __restrict__ counts,
+                                                                            int32_t* __restrict__ perm)
+{
+    constexpr int kParts = kScatThreads / kBuckets;
+    __shared__ uint32_t tot[kParts][kBuckets], pre[kParts][kBuckets];
+    __shared__ uint32_t start[kBuckets];
+    __shared__ uint32_t cur[kBuckets];
+    const int t = threadIdx.x;
+    const int c = blockIdx.x;
+    const int k = t % kBuckets, part = t / kBuckets;
+    uint32_t all = 0, before = 0;
+    for (int ch = part; ch < nch; ch += kParts) {
+        const uint32_t v = counts[(long long)ch * kBuckets + k];
+        all += v;
+        before += ch < c ? v : 0u;
+    }
+    tot[part][k] = all;
+    pre[part][k] = before;
+    __syncthreads();
+    uint32_t mine = 0;
+    if (t < kBuckets) {
+        uint32_t a = 0;
+#pragma unroll
+        for (int q = 0; q < kParts; ++q) { a += tot[q][t]; mine += pre[q][t]; }
+        start[t] = a;
+    }
+    __syncthreads();
+    for (int o = 1; o < kBuckets; o <<= 1) {  // inclusive scan of the bucket totals, heaviest first
+        const uint32_t add = (t < kBuckets && t >= o) ? start[t - o] : 0u;
+        __syncthreads();
+        if (t < kBuckets) start[t] += add;
+        __syncthreads();
+    }
+    if (t < kBuckets) cur[t] = (t ? start[t - 1] : 0u) + mine;
+    __syncthreads();
+    const long long r0 = (long long)c * chunk;
+    const long long r1 = r0 + chunk < B ? r0 + chunk : B;
+    for (long long b = r0 + t; b < r1; b += kScatThreads) perm[atomicAdd(&cur[key[b]], 1u)] = (int32_t)b;
+}
+
 // rows per chunk: at least min_chunk (one pass of the histogram workgroup), enough that there
 // are at most kMaxChunks chunks
-static int chunk_of(long long B, int min_chunk, int* nchunks)
+// and, below that, about QEC_SCHED_TARGET_CHUNKS chunks (power-of-two sizes up to max_chunk), so a small
+// batch still spreads its histogram over many workgroups (P7 65 536 at the fixed 4096 rows per chunk:
+// 16 workgroups, 36 us)
+static int chunk_of(long long B, int min_chunk, int max_chunk, int* nchunks)
 {
     long long chunk = (B + kMaxChunks - 1) / kMaxChunks;
-    if (chunk < min_chunk) chunk = min_chunk;
+    long long want = min_chunk;
+    while (want < max_chunk && want * QEC_SCHED_TARGET_CHUNKS < B) want *= 2;
+    if (chunk < want) chunk = want;
     *nchunks = (int)((B + chunk - 1) / chunk);
     return (int)chunk;
 }
@@ -223,7 +282,11 @@ int launch_schedule(const uint8_t* sX, const uint8_t* sZ, bool sbits, long long 
     // short rows: 4096 syndromes per chunk (four per thread): the offsets and scatter passes then
     // handle a quarter of the chunks (P7 2^20: order pass 60 -> 51 us, profiles/r02/hist_ab_r02s3zj.txt;
     // staging the rows through LDS did not speed the histogram up)
-    const int chunk = chunk_of(B, shortrows ? 4 * kHistThreads : 256, &nch);
+    const int split = shortrows ? 1 : kHistSplitLong;
+    const int chunk = chunk_of(B, 256, shortrows ? 4 * kHistThreads : 512, &nch);
+    // histogram workgroup: one pass over its chunk when the chunk is small (256 .. 1024 threads)
+    int hthreads = chunk * split;
+    hthreads = hthreads < 256 ? 256 : hthreads > kHistThreads ? kHistThreads : (hthreads + 63) / 64 * 64;
     uint8_t* p = static_cast<uint8_t*>(ws);
     int32_t* perm = reinterpret_cast<int32_t*>(p);
     uint32_t* counts = reinterpret_cast<uint32_t*>(p + perm_bytes(B));
@@ -231,18 +294,23 @@ int launch_schedule(const uint8_t* sX, const uint8_t* sZ, bool sbits, long long 
     uint8_t* key = reinterpret_cast<uint8_t*>(totals + kBuckets);
     *perm_out = perm;
     if (sbits)
-        hipLaunchKernelGGL(schedule_hist_bits_kernel, dim3(nch), dim3(kHistThreads), 0, st,
+        hipLaunchKernelGGL(schedule_hist_bits_kernel, dim3(nch), dim3(hthreads), 0, st,
                            reinterpret_cast<const uint32_t*>(sX), reinterpret_cast<const uint32_t*>(sZ), B, (mX + 31) / 32,
                            (mZ + 31) / 32, chunk, key, counts, zero_merge);
     else if (shortrows)
-        hipLaunchKernelGGL(schedule_hist_kernel<1>, dim3(nch), dim3(kHistThreads), 0, st, sX, sZ, B, mX, mZ, chunk, key,
+        hipLaunchKernelGGL(schedule_hist_kernel<1>, dim3(nch), dim3(hthreads), 0, st, sX, sZ, B, mX, mZ, chunk, key,
                            counts, zero_merge);
     else
-        hipLaunchKernelGGL(schedule_hist_kernel<kHistSplitLong>, dim3(nch), dim3(kHistThreads), 0, st, sX, sZ, B, mX, mZ,
+        hipLaunchKernelGGL(schedule_hist_kernel<kHistSplitLong>, dim3(nch), dim3(hthreads), 0, st, sX, sZ, B, mX, mZ,
                            chunk, key, counts, zero_merge);
-    hipLaunchKernelGGL(schedule_offsets_kernel, dim3(kBuckets), dim3(kScanThreads), 0, st, nch, counts, totals);
-    hipLaunchKernelGGL(schedule_scatter_kernel, dim3(nch), dim3(kScatThreads), 0, st, key, B, chunk, counts, totals,
-                       perm);
+    if (nch <= kMaxFusedChunks) {
+        hipLaunchKernelGGL(schedule_scatter_fused_kernel, dim3(nch), dim3(kScatThreads), 0, st, key, B, chunk, nch, counts,
+                           perm);
+    } else {
+        hipLaunchKernelGGL(schedule_offsets_kernel, dim3(kBuckets), dim3(kScanThreads), 0, st, nch, counts, totals);
+        hipLaunchKernelGGL(schedule_scatter_kernel, dim3(nch), dim3(kScatThreads), 0, st, key, B, chunk, counts, totals,
+                           perm);
+    }
     const hipError_t err = hipGetLastError();
     if (err != hipSuccess) return fail(QEC_ERR_HIP, std::string("schedule launch: ") + hipGetErrorString(err));
     return QEC_OK;

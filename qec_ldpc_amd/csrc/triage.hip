@@ -1,0 +1,249 @@
+// Iteration-0 triage for the syndrome stop rule (hard part 3: active-syndrome
+// compaction), on the Monte-Carlo pipeline's bit-row syndromes.
+//
+// Under QEC_STOP_SYNDROME a sector stops after the first iteration whose hard decision satisfies its
+// syndrome.  Iteration 0 starts from q = p' on every edge (DecoderCPU.h:265-267), so after it a
+// variable's R outgoing messages, hence its hard decision (DecoderCPU.h:354-373) and whether they all
+// lie outside (0.01, 0.99) (:231-246), depend only on the R-bit pattern of its checks' syndrome bits
+// (bp_decode.hip, iteration0 / pattern_masks): two 2^R-bit masks, hdpat and cvpat, computed on the
+// host from the iteration-0 table with the same float compares.  At low p nearly every sector stops
+// there (P61 at p = 0.002: 99 %), yet the decode kernel spends a whole wave (one syndrome) on it.
+//
+// This kernel decides iteration 0 for 64 syndromes per wave, one lane per syndrome, bit-sliced over
+// the P variables of a circulant block: with s_r the P syndrome bits of block row r (bit i = check
+// (r, i)), the pattern bit r of variable (l, j) is bit j of rotl(s_r, E[r][l]) (check (r, (j - E) mod P)),
+// the block's decisions are hdpat evaluated on those R words (a multiplexer tree, v_bfi), and the
+// decision's syndrome on check (r, i) is bit i of XOR_l rotr(hd_l, E[r][l]).  A sector whose syndrome
+// matches stops: its record bytes, iteration count (1) and flags are final -- exactly the outputs the
+// decode kernel produces for it (tests/test_gpu_triage.py checks that bit for bit).  The others are
+// appended to per-sector lists that the decode kernel's list mode then decodes from scratch; the two
+// sectors of a syndrome meet in its merge word as in the sector-split launches (done bit + flags).
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "qec_device.h"
+#include "qec_internal.h"
+
+namespace qec {
+
+constexpr int kTriageWaves = 4;
+constexpr int kTriageMaxRL = 128;
+
+struct TriageArgs {
+    const uint32_t* sX;  // [B][wX] bit rows (bit c = check c)
+    const uint32_t* sZ;  // [B][wZ]
+    long long B;
+    int wX, wZ, nb, recB;
+    uint32_t hdpatX, cvpatX, hdpatZ, cvpatZ;  // bit idx: pattern idx decides 1 / stays outside (0.01, 0.99)
+    uint8_t* rec;        // [B][recB] decision records
+    int32_t* iters;      // [B][2] or null
+    uint32_t* merge;     // [B]: done bit (0x100 X, 0x200 Z) + that sector's flags
+    int32_t* listX;      // [B] syndromes whose X sector goes on
+    int32_t* listZ;
+    uint32_t* counts;    // [2] list lengths (zeroed before the launch)
+    int EX[kTriageMaxRL], EZ[kTriageMaxRL];
+};
+
+template <int P>
+__device__ __forceinline__ uint64_t rotl(uint64_t x, int k)
+{
+    constexpr uint64_t mask = P >= 64 ? ~0ull : (1ull << P) - 1ull;
+    return k == 0 ? x : ((x << k) | (x >> (P - k))) & mask;
+}
+template <int P>
+__device__ __forceinline__ uint64_t rotr(uint64_t x, int k)
+{
+    constexpr uint64_t mask = P >= 64 ? ~0ull : (1ull << P) - 1ull;
+    return k == 0 ? x : ((x >> k) | (x << (P - k))) & mask;
+}
+
+// f(idx_j) bit-sliced over the P variables: bit j of the result = bit idx_j of pat, idx_j = the bits j
+// of v[0..R) (v[r] -> bit r).  A multiplexer tree over v[0] .. v[R-1] (one v_bfi per node and half).
+template <int R>
+__device__ __forceinline__ uint64_t pattern_eval(uint32_t pat, const uint64_t (&v)[R])
+{
+    uint64_t t[1 << (R - 1)];
+#pragma unroll
+    for (int m = 0; m < (1 << (R - 1)); ++m) {
+        const uint64_t c0 = 0ull - (uint64_t)((pat >> (2 * m)) & 1u), c1 = 0ull - (uint64_t)((pat >> (2 * m + 1)) & 1u);
+        t[m] = (v[0] & c1) | (~v[0] & c0);
+    }
+#pragma unroll
+    for (int j = 1; j < R; ++j)
+#pragma unroll
+        for (int m = 0; m < (1 << (R - 1 - j)); ++m) t[m] = (v[j] & t[2 * m + 1]) | (~v[j] & t[2 * m]);
+    return t[0];
+}
+
+// One sector of this lane's syndrome (its bit row): the decisions hd[l] (bit j = variable (l, j)),
+// whether iteration 0 satisfies the syndrome, and whether some message lies inside (0.01, 0.99).
+template <int R, int L, int P>
+__device__ __forceinline__ bool triage_sector(const uint32_t* __restrict__ row, const int* E, uint32_t hdpat,
+                                              uint32_t cvpat, uint64_t (&hd)[L], bool& cvbad)
+{
+    static_assert(R <= 5 && P <= 64, "patterns in 32 bits, blocks in 64");
+    constexpr uint64_t mask = P >= 64 ? ~0ull : (1ull << P) - 1ull;
+    constexpr int kW = (R * P + 31) / 32;  // words of the row
+    constexpr uint32_t full = R >= 5 ? 0xFFFFFFFFu : (1u << (1 << R)) - 1u;
+    uint32_t w[kW + 2];
+#pragma unroll
+    for (int k = 0; k < kW; ++k) w[k] = row[k];
+    w[kW] = 0u;
+    w[kW + 1] = 0u;
+    uint64_t s[R];  // block row r: bit i = check (r, i)
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int o = r * P, k = o >> 5, sh = o & 31;
+        const uint64_t lo = (uint64_t)w[k] | ((uint64_t)w[k + 1] << 32);
+        const uint64_t v = sh == 0 ? lo : (lo >> sh) | ((uint64_t)w[k + 2] << (64 - sh));
+        s[r] = v & mask;
+    }
+    const bool hd_const = hdpat == 0u || hdpat == full;  // uniform: no tree needed
+    uint64_t bad = 0;
+#pragma unroll
+    for (int l = 0; l < L; ++l) {
+        uint64_t v[R];  // bit j: syndrome bit of check (r, (j - E[r][l]) mod P) of variable (l, j)
+#pragma unroll
+        for (int r = 0; r < R; ++r) v[r] = rotl<P>(s[r], E[r * L + l]);
+        hd[l] = hd_const ? (hdpat ? mask : 0ull) : (pattern_eval<R>(hdpat, v) & mask);
+        if (cvpat != full) bad |= pattern_eval<R>(~cvpat, v);
+    }
+    cvbad = (bad & mask) != 0ull;
+    bool ok = true;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {  // syndrome of the decision: check (r, i) XORs variables (l, (E + i) mod P)
+        uint64_t par = 0;
+#pragma unroll
+        for (int l = 0; l < L; ++l) par ^= rotr<P>(hd[l], E[r * L + l]);
+        ok &= par == s[r];
+    }
+    return ok;
+}
+
+// this lane's sector decisions as nb record bytes (bit l P + j of the sector = variable (l, j), bit
+// k of byte t = qubit 8 t + k), into its row of the wave's LDS stage
+template <int L, int P>
+__device__ __forceinline__ void stage_sector(uint8_t* __restrict__ row, int nb, const uint64_t (&hd)[L])
+{
+    uint64_t acc = 0;  // pending bits (have < 8 of them between blocks)
+    int have = 0, out = 0;
+#pragma unroll
+    for (int l = 0; l < L; ++l) {
+        uint64_t lo = acc | (hd[l] << have);
+        uint64_t hi = have ? hd[l] >> (64 - have) : 0ull;  // the block's bits past 64 (P + have > 64)
+        int tot = have + P;
+        while (tot >= 8) {
+            row[out++] = (uint8_t)lo;
+            lo = (lo >> 8) | (hi << 56);
+            hi >>= 8;
+            tot -= 8;
+        }
+        acc = lo;
+        have = tot;
+    }
+    if (have > 0) row[out++] = (uint8_t)acc;
+    for (; out < nb; ++out) row[out] = 0;
+}
+
+template <int J, int K, int L, int P>
+__global__ __launch_bounds__(64 * kTriageWaves) void triage_kernel(const TriageArgs a)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t tri_smem[];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int recB = a.recB, nb = a.nb;
+    uint8_t* __restrict__ stage = tri_smem + (size_t)wv * (64 * recB + 16);
+    const long long b0 = ((long long)blockIdx.x * kTriageWaves + wv) * 64;
+    if (b0 >= a.B) return;
+    const int ns = (int)(a.B - b0 < 64 ? a.B - b0 : 64);
+    const long long b = b0 + lane;
+    const bool valid = lane < ns;
+    const long long bl = valid ? b : b0;  // clamped row (its results are discarded)
+    uint64_t hdX[L], hdZ[L];
+    bool cvbX = false, cvbZ = false;
+    const bool okX = triage_sector<J, L, P>(a.sX + bl * a.wX, a.EX, a.hdpatX, a.cvpatX, hdX, cvbX);
+    const bool okZ = triage_sector<K, L, P>(a.sZ + bl * a.wZ, a.EZ, a.hdpatZ, a.cvpatZ, hdZ, cvbZ);
+    const bool doneX = valid && okX, doneZ = valid && okZ;
+    const uint32_t fX = cvbX ? QEC_CONVERGENCE_FAIL_X : 0u, fZ = cvbZ ? QEC_CONVERGENCE_FAIL_Z : 0u;
+    // record rows: both sectors' decisions (a sector that goes on is overwritten by the list decode),
+    // the flags byte final when both stopped (else written by the list decode's merge)
+    uint8_t* __restrict__ my = stage + lane * recB;
+    if (valid) {
+        stage_sector<L, P>(my, nb, hdX);
+        stage_sector<L, P>(my + nb, nb, hdZ);
+        my[2 * nb] = (uint8_t)(fX | fZ);
+    }
+    wave_sync();
+    // the wave's contiguous block of records: 16-byte stores over its aligned body, bytes at the ends
+    {
+        uint8_t* __restrict__ g = a.rec + b0 * recB;
+        const int tot = ns * recB;
+        const uintptr_t g0 = reinterpret_cast<uintptr_t>(g);
+        const int head = (int)min((uintptr_t)tot, (16 - (g0 & 15)) & 15);
+        const int body = (tot - head) >> 4;
+        const int tail0 = head + 16 * body;
+        if (lane < head) g[lane] = stage[lane];
+        for (int t = lane; t < body; t += 64) {
+            const int o = head + 16 * t;
+            uint32_t w4[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                w4[q] = (uint32_t)stage[o + 4 * q] | (uint32_t)stage[o + 4 * q + 1] << 8 |
+                        (uint32_t)stage[o + 4 * q + 2] << 16 | (uint32_t)stage[o + 4 * q + 3] << 24;
+            *reinterpret_cast<uint4*>(g + o) = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+        }
+        if (tail0 + lane < tot) g[tail0 + lane] = stage[tail0 + lane];
+    }
+    if (valid) {
+        if (a.iters != nullptr) *reinterpret_cast<int2*>(a.iters + 2 * b) = make_int2(1, 1);  // list sectors rewrite theirs
+        a.merge[b] = (doneX ? 0x100u | fX : 0u) | (doneZ ? 0x200u | fZ : 0u);
+    }
+    // sectors that go on: appended to the lists (one atomic per wave and sector)
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    const unsigned long long gx = __ballot(valid && !okX), gz = __ballot(valid && !okZ);
+    uint32_t baseX = 0, baseZ = 0;
+    if (lane == 0) {
+        if (gx) baseX = atomicAdd(&a.counts[0], (uint32_t)__popcll(gx));
+        if (gz) baseZ = atomicAdd(&a.counts[1], (uint32_t)__popcll(gz));
+    }
+    baseX = __shfl(baseX, 0);
+    baseZ = __shfl(baseZ, 0);
+    if ((gx >> lane) & 1ull) a.listX[baseX + __popcll(gx & lt)] = (int32_t)b;
+    if ((gz >> lane) & 1ull) a.listZ[baseZ + __popcll(gz & lt)] = (int32_t)b;
+}
+
+using TriageFn = void (*)(const TriageArgs);
+
+static TriageFn triage_fn(const Code& c)
+{
+    if (c.J == 4 && c.K == 5 && c.L == 10 && c.P == 61) return triage_kernel<4, 5, 10, 61>;
+    if (c.J == 3 && c.K == 3 && c.L == 6 && c.P == 7) return triage_kernel<3, 3, 6, 7>;
+    return nullptr;
+}
+
+bool triage_supported(const Code& c) { return c.is_qc && triage_fn(c) != nullptr; }
+
+int launch_triage(const Code& c, const uint32_t* sX, const uint32_t* sZ, long long B, const uint32_t pats[4],
+                  uint8_t* rec, int32_t* iters, uint32_t* merge, int32_t* listX, int32_t* listZ, uint32_t* counts,
+                  hipStream_t st)
+{
+    TriageFn fn = triage_fn(c);
+    if (!fn) return fail(QEC_ERR_UNSUPPORTED, "triage: no kernel for this code");
+    if (B <= 0) return QEC_OK;
+    TriageArgs a{};
+    a.sX = sX; a.sZ = sZ; a.B = B;
+    a.wX = (c.mX + 31) / 32; a.wZ = (c.mZ + 31) / 32;
+    a.nb = (c.n + 7) / 8; a.recB = 2 * a.nb + 1;
+    a.hdpatX = pats[0]; a.cvpatX = pats[1]; a.hdpatZ = pats[2]; a.cvpatZ = pats[3];
+    a.rec = rec; a.iters = iters; a.merge = merge; a.listX = listX; a.listZ = listZ; a.counts = counts;
+    for (size_t k = 0; k < c.EX.size(); ++k) a.EX[k] = c.EX[k];
+    for (size_t k = 0; k < c.EZ.size(); ++k) a.EZ[k] = c.EZ[k];
+    const long long per_block = 64LL * kTriageWaves;
+    const size_t smem = (size_t)kTriageWaves * (64 * a.recB + 16);
+    hipLaunchKernelGGL(fn, dim3((unsigned)((B + per_block - 1) / per_block)), dim3(64 * kTriageWaves), smem, st, a);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(QEC_ERR_HIP, std::string("triage launch: ") + hipGetErrorString(e));
+    return QEC_OK;
+}
+
+}  // namespace qec

@@ -87,3 +87,34 @@ def test_decodercpu_header_builds_main_loop(tmp_path, code_paths):
     r = subprocess.run([str(exe), code_paths["P7"]], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr
     assert "Errors Tested: " in r.stdout and "Rand Seed: 2881811342" in r.stdout
+
+
+@pytest.mark.parametrize("key", ["P7", "P61"])
+@pytest.mark.parametrize("stop", ["ref", "fixed", "syndrome"])
+def test_non_binary_syndrome_entries(env, key, stop):
+    """Syndrome entries other than 0 / 1 keep the reference's two readings: the check update takes
+    their truthiness (DecoderCPU.h:178) and the syndrome comparison their exact value (:381), so
+    such a sector decodes as with a 1 there and always reports SYNDROME_FAIL (oracle semantics)."""
+    code, dec, orc = env[key]
+    B = 40 if key == "P61" else 200
+    x, z = depolarizing_errors(code.n, 4242, B, 0.02)
+    sX, sZ = code.syndrome(0, x), code.syndrome(1, z)
+    rng = np.random.default_rng(9)
+    for s in (sX, sZ):
+        rows = rng.choice(B, B // 3, replace=False)
+        cols = rng.integers(0, s.shape[1], B // 3)
+        s[rows, cols] = rng.choice(np.array([2, 3, 128, 255], np.uint8), B // 3)
+    g = dec.decode_batch(sX, sZ, 0.02, 12, stop, want_iters=True, want_q=True)
+    o = orc.decode_batch(sX, sZ, 0.02, 12, stop, want_q=True)
+    for name, a, b in zip(("eX", "eZ", "flags", "iters"), g[:4], o[:4]):
+        assert np.array_equal(a, b), name
+    assert same_floats(g[4], o[4])
+    bad = (sX > 1).any(1)
+    assert (g[2][bad] & 1).all()  # SYNDROME_FAIL_X wherever an X entry is not 0 / 1
+    # Decoder::Decode with int entries (256 would wrap to 0 as a byte): 0 / 1 / other
+    b = int(np.nonzero(bad)[0][0])
+    sx = sX[b].astype(np.int32)
+    sx[sx > 1] = 256
+    f, ex, ez = dec.Decode(sx, sZ[b].astype(np.int32), 0.02, 12)
+    r = orc.decode_batch(sX[b:b + 1], sZ[b:b + 1], 0.02, 12, "ref")  # Decode is the reference stop rule
+    assert f == r[2][0] and np.array_equal(ex, r[0][0]) and np.array_equal(ez, r[1][0])

@@ -28,8 +28,13 @@ def run(request, code_paths):
 
 
 def test_oracle_subsample(run):
-    rng = np.random.default_rng(123)
-    idx = np.sort(rng.choice(run["B"], 256, replace=False))
+    """configs[1] (P7, ~0.1 s of oracle time): the whole batch; configs[2]: a 4 096-syndrome slice
+    plus 256 syndromes drawn from the whole batch."""
+    if run["key"] == "P7":
+        idx = np.arange(run["B"])
+    else:
+        rng = np.random.default_rng(123)
+        idx = np.unique(np.concatenate([np.arange(20000, 20000 + 4096), rng.choice(run["B"], 256, replace=False)]))
     o = OracleCode(run["path"]).decode_batch(run["sX"][idx], run["sZ"][idx], run["p"], run["N"], "fixed")
     for a, b in zip(run["out"][:4], o[:4]):
         assert np.array_equal(a[idx], b)
@@ -124,8 +129,9 @@ def mega(code_paths):
 
 
 def test_configs3_oracle_subsample(mega):
+    """A 4 096-syndrome slice at the end of the batch plus 192 syndromes drawn from all of it."""
     rng = np.random.default_rng(2020)
-    idx = np.sort(rng.choice(mega["B"], 192, replace=False))
+    idx = np.unique(np.concatenate([np.arange(mega["B"] - 4096, mega["B"]), rng.choice(mega["B"], 192, replace=False)]))
     sX = mega["sX"].cpu().numpy()[idx]
     sZ = mega["sZ"].cpu().numpy()[idx]
     o = OracleCode(mega["path"]).decode_batch(sX, sZ, 0.01, 50, "fixed")

@@ -109,6 +109,25 @@ def test_monte_carlo_shards_add_up(env):
         assert whole[k] == a[k] + b[k], k
 
 
+def test_monte_carlo_full_batch(env):
+    """qec_monte_carlo at psweep's default shape (2^20 samples in one batch: 64-lane front-end waves,
+    one decode launch) against oracle counting on its last 2 048 samples (the same launch shape minus
+    them covers the rest), and eight contiguous shards adding up to it (BASELINE configs[4]/[5])."""
+    code, dec, orc = env["P61"]
+    B, p, tail, seed = 1 << 20, 0.005, 2048, 0x51EC0DE
+    whole = dec.monte_carlo(seed, 0, B, p, 50, "syndrome")
+    head = dec.monte_carlo(seed, 0, B - tail, p, 50, "syndrome")
+    x, z = depolarizing(seed, B - tail, tail, code.n, p)
+    exp, it = oracle_counters(orc, x, z, p, 50, "syndrome")
+    for k in q.MC_COUNTERS:
+        assert whole[k] == head[k] + exp[k], k
+    assert whole["iterationsX"] == head["iterationsX"] + int(it[:, 0].sum())
+    assert whole["iterationsZ"] == head["iterationsZ"] + int(it[:, 1].sum())
+    parts = [dec.monte_carlo(seed, g * B // 8, B // 8, p, 50, "syndrome") for g in range(8)]
+    for k in q.MC_COUNTERS + ("tested", "iterationsX", "iterationsZ"):
+        assert whole[k] == sum(r[k] for r in parts), k
+
+
 @pytest.mark.parametrize("key", ["P7", "P61"])
 def test_pack_decisions_matches_host(env, key):
     """qec_pack_decisions_dev (the gather payload) equals the host packing of

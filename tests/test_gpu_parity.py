@@ -94,7 +94,7 @@ def test_ragged_batches(env, B):
 
 
 @pytest.mark.parametrize("key", ["P7", "P61"])
-@pytest.mark.parametrize("p", [0.001, 0.002, 0.01, 0.05])
+@pytest.mark.parametrize("p", [0.001, 0.002, 0.005, 0.01, 0.05])
 def test_syndrome_stop_without_messages(env, key, p):
     """The syndrome stop's shortcuts that apply only when no final messages are requested: a
     sector with a zero syndrome skips to its known outputs, and iteration 0 tests the syndrome
@@ -353,3 +353,32 @@ def test_schedule_covers_every_syndrome(env, key, B):
     assert int(outs[0][3].min()) >= 1  # batch order wrote every syndrome
     for name, a, b in zip(("eX", "eZ", "flags", "iters"), outs[0], outs[1]):
         assert torch.equal(a, b), "%s B=%d: %s differs between batch and dispatch order" % (key, B, name)
+
+
+@pytest.mark.parametrize("key", ["P7", "P61"])
+@pytest.mark.parametrize("engine", ["circulant", "sparse"])
+@pytest.mark.parametrize("stop", ["ref", "fixed", "syndrome"])
+def test_non_binary_syndrome_entries(env, key, engine, stop):
+    """Syndrome bytes other than 0 / 1: the check update takes their truthiness (DecoderCPU.h:178),
+    the syndrome tests their exact value (:381) -- such a sector decodes as with a 1 there and
+    always reports SYNDROME_FAIL; the syndrome stop never stops on it.  Against the oracle, with
+    and without final messages (the syndrome stop's message-free shortcuts)."""
+    code, _, orc = env[key]
+    dec = q.DecoderGPU(code, 0, engine=engine)
+    B = 64 if key == "P61" else 500
+    x, z = depolarizing_errors(code.n, 4242, B, 0.02)
+    sX, sZ = code.syndrome(0, x), code.syndrome(1, z)
+    rng = np.random.default_rng(9)
+    for s in (sX, sZ):
+        rows = rng.choice(B, B // 3, replace=False)
+        s[rows, rng.integers(0, s.shape[1], B // 3)] = rng.choice(np.array([2, 3, 128, 255], np.uint8), B // 3)
+    sX[-1] = 0
+    sX[-1, 0] = 7  # otherwise-zero syndrome with one non-binary entry
+    for want_q in (True, False):
+        g = dec.decode_batch(sX, sZ, 0.02, 12, stop, want_iters=True, want_q=want_q)
+        o = orc.decode_batch(sX, sZ, 0.02, 12, stop, want_q=want_q)
+        for name, a, b in zip(("eX", "eZ", "flags", "iters"), g[:4], o[:4]):
+            assert np.array_equal(a, b), (name, want_q)
+        if want_q:
+            assert same_floats(g[4], o[4])
+    assert (g[2][(sX > 1).any(1)] & 1).all()

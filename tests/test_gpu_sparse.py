@@ -122,6 +122,38 @@ def test_large_circulant_code(tmp_path, J, K, L, P, s, t, mode):
         compare(g, o, "P=%d %s" % (P, stop))
 
 
+def test_large_code_front_end_full_width(tmp_path):
+    """The fused front end's samples per wave are capped by the LDS the gap table leaves
+    (montecarlo.hip launch_mc_gap): the n = 762 code (72 words of sample state) at 2^19 samples
+    runs at 54 instead of 64 per wave and draws the same samples as a 1000-sample launch and the
+    numpy restatement of the Philox stream; monte_carlo at that batch equals its 8192 batches."""
+    import torch
+    from oracle.philox import depolarizing
+    _, code = generated_file(tmp_path, 3, 3, 6, 127, 2, 3)
+    dec = q.DecoderGPU(code, 0)
+    dev = torch.device("cuda", 0)
+    nb2 = 2 * ((code.n + 7) // 8)
+
+    def bufs(B):
+        return [torch.empty((B, w), dtype=torch.uint8, device=dev) for w in (code.numEqsX, code.numEqsZ, nb2)]
+
+    B, lo, seed, p = 1 << 19, 300001, 5, 0.01
+    big, small = bufs(B), bufs(1000)
+    dec.sample_syndrome_dev(seed, 0, p, *big)
+    dec.sample_syndrome_dev(seed, lo, p, *small)
+    torch.cuda.synchronize()
+    for a, b in zip(big, small):
+        assert torch.equal(a[lo:lo + 1000], b)
+    x, z = depolarizing(seed, lo, 1000, code.n, p)
+    assert np.array_equal(small[0].cpu().numpy(), code.syndrome(0, x))
+    assert np.array_equal(small[1].cpu().numpy(), code.syndrome(1, z))
+    a = dec.monte_carlo(seed, 0, B, p, 20, "syndrome", batch=B)
+    b = dec.monte_carlo(seed, 0, B, p, 20, "syndrome", batch=8192)
+    for k in ("tested", "withX", "withZ", "synX", "synZ", "logical", "corrected", "convX", "convZ",
+              "iterationsX", "iterationsZ"):
+        assert a[k] == b[k], (k, a[k], b[k])
+
+
 def test_irregular_code_is_rejected(code_paths, tmp_path):
     c = q.Quantum_LDPC_Code.createFromFile(code_paths["P7"])
     HX = c.pcm(0).copy()

@@ -19,6 +19,7 @@ Usage: python tools/gpu/pmc_summary.py --dir gpurun_out/prof_TAG/p61 --code p61
 import argparse
 import csv
 import glob
+import hashlib
 import json
 import os
 
@@ -86,6 +87,11 @@ def main():
            "kernel_trace_avg_ns": dur_ns, "kernel_trace_dispatches": len(durs)}
     per_launch = {k: round(v) for k, v in avg.items()}
     out["per_launch"] = per_launch
+    # the library the counters were collected on: bench.py uses this profile only for that binary
+    lib = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))),
+                       "qec_ldpc_amd", "libqecldpc.so")
+    with open(lib, "rb") as fh:
+        out["library_sha256"] = hashlib.sha256(fh.read()).hexdigest()
     if "FETCH_SIZE" in avg and "WRITE_SIZE" in avg:
         hbm = 2.0 * avg["FETCH_SIZE"] * 1024.0 + avg["WRITE_SIZE"] * 1024.0
         out["hbm_bytes_per_launch"] = round(hbm)

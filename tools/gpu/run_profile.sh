@@ -2,6 +2,7 @@
 # PMC passes (each counter group in its own run, --kernel-trace only beside --pmc), then the
 # per-launch / per-syndrome summary bench.py reads (profiles/pmc_<code>.json).
 #   bash tools/gpu/run_profile.sh TAG [codes...]
+# EXTRA="--global-batch 65536" profiles another workload of bench.py (same per-code layout).
 set -o pipefail
 R="$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
@@ -11,7 +12,7 @@ OUT="$R/gpurun_out/prof_$TAG"
 mkdir -p "$OUT"; cd /tmp
 for code in $CODES; do
   mkdir -p "$OUT/$code"
-  BENCH="$R/bench.py --no-cpu --no-extras --code $code"
+  BENCH="$R/bench.py --no-cpu --no-extras --code $code $EXTRA"
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/$code/trace" -o run -- \
       python3 $BENCH --steps 10 --warmup 2 > "$OUT/$code/bench_trace.json" 2> "$OUT/$code/trace.err"
   rc=$?; echo "$code trace rc=$rc"; cat "$OUT/$code/bench_trace.json"

@@ -19,6 +19,7 @@ common qec_ldpc_amd/csrc/montecarlo.hip &
 common qec_ldpc_amd/csrc/capi.cpp -x hip &
 common qec_ldpc_amd/csrc/bp_sparse.hip &
 common qec_ldpc_amd/csrc/schedule.hip &
+common qec_ldpc_amd/csrc/triage.hip &
 wait
 build() {
   name=$1; shift

@@ -18,7 +18,7 @@ from qec_ldpc_amd.codes import P7, P61, code_path  # noqa: E402
 from qec_ldpc_amd.synthetic import depolarizing_errors  # noqa: E402
 
 CODES = {"p61": (P61, 0.01, 50), "p7": (P7, 0.02, 20)}
-OPTIONS = {"hard_paths": 1, "cycle_jump": 2, "schedule": 3, "sector_split": 4, "phase_stats": 5}
+OPTIONS = {"hard_paths": 1, "cycle_jump": 2, "schedule": 3, "sector_split": 4, "phase_stats": 5, "triage": 6}
 
 
 def bind(path):

@@ -20,6 +20,18 @@ __device__ __forceinline__ f2 pk_mul(f2 a, f2 b)
     asm volatile("v_pk_mul_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
     return r;
 }
+__device__ __forceinline__ f2 pk_fma(f2 a, f2 b, f2 c)
+{
+    f2 r;
+    asm volatile("v_pk_fma_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+__device__ __forceinline__ f2 pk_add(f2 a, f2 b)
+{
+    f2 r;
+    asm volatile("v_pk_add_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
 __device__ __forceinline__ float mul(float a, float b)
 {
     float r;
@@ -73,7 +85,8 @@ __device__ __forceinline__ float bperm(float a, int addr)
 // OP 0: v_mul_f32, 1: v_pk_mul_f32 (2 fp32 products / lane), 2: v_rcp_f32,
 // 3: IEEE fp32 division as hipcc emits it (11 instructions), counted per division,
 // 4: v_fma_f32, 5: v_add_f32, 6: v_div_scale_f32, 7: v_div_fixup_f32,
-// 8: v_div_fmas_f32 (+ one s_mov_b64 vcc each).
+// 8: v_div_fmas_f32 (+ one s_mov_b64 vcc each), 9: ds_bpermute_b32, 10: 1 ds_bpermute + NCH-1 v_mul,
+// 11: v_pk_fma_f32, 12: v_pk_add_f32, 13: v_mul / v_rcp alternating, 14: 1 v_rcp per 4 v_mul.
 template <int OP, int NCH>
 __global__ __launch_bounds__(256) void probe(long long* cycles, float a)
 {
@@ -101,6 +114,12 @@ __global__ __launch_bounds__(256) void probe(long long* cycles, float a)
             if (OP == 8) x[c] = dfmas(x[c], a, 0.0001f);
             if (OP == 9) x[c] = bperm(x[c], (int)((threadIdx.x * 4 + 4 * (c + 1)) & 255));
             if (OP == 10) x[c] = c == 0 ? bperm(x[c], (int)((threadIdx.x * 4 + 4) & 255)) : mul(x[c], a);
+            if (OP == 11) y[c] = pk_fma(y[c], a2, f2{0.0001f, 0.0002f});
+            if (OP == 12) y[c] = pk_add(y[c], a2);
+            // half the chains v_mul_f32, half v_rcp_f32 (does the transcendental overlap plain VALU?)
+            if (OP == 13) x[c] = (c & 1) ? rcp(x[c]) : mul(x[c], a);
+            // 1 v_rcp_f32 per 4 v_mul_f32 (about the division mix of the var pass)
+            if (OP == 14) x[c] = (c % 5 == 0) ? rcp(x[c]) : mul(x[c], a);
         }
     }
     const long long t1 = __builtin_amdgcn_s_memtime();
@@ -111,7 +130,9 @@ __global__ __launch_bounds__(256) void probe(long long* cycles, float a)
 }
 
 static double g_mhz = 0;  // s_memtime ticks per microsecond of the last timed launch
+static double g_ev = 0;   // the last timed launch by HIP events: SIMD-cycles per wave-instruction at 2.4 GHz
 
+static int cus_g = 256;
 template <int OP, int NCH>
 static double run(long long* d, int blocks, std::vector<long long>& h, int wps = 8)
 {
@@ -134,6 +155,9 @@ static double run(long long* d, int blocks, std::vector<long long>& h, int wps =
     long long mx = 0;
     for (size_t k = 0; k < nw; ++k) mx = h[k] > mx ? h[k] : mx;
     g_mhz = mx / (ms * 1e3);  // the longest wave spans ~the whole launch
+    // launch time (events, includes launch overhead and the wave start/finish ramp) in 2.4 GHz
+    // cycles over the instructions each SIMD issued: an upper bound on the per-instruction cost
+    g_ev = (ms * 1e-3 * 2.4e9) / ((double)wps * kIters * NCH) * ((double)cus_g * 4 * wps / ((double)blocks * 4));
     // 8 waves share each SIMD for the whole run: SIMD-cycles per wave-instruction
     return mean_wave_cycles / ((double)wps * kIters * NCH);
 }
@@ -142,19 +166,24 @@ int main()
 {
     int cus = 0;
     hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
+    cus_g = cus;
     const int blocks = cus * 8;  // 32 waves per CU = 8 per SIMD
     long long* d = nullptr;
     hipMalloc(&d, sizeof(long long) * blocks * 4);
     std::vector<long long> h((size_t)blocks * 4);
     printf("{\"cus\": %d, \"waves_per_simd\": 8", cus);
     printf(", \"v_mul_f32 x8\": %.3f", run<0, 8>(d, blocks, h));
+    printf(", \"v_mul_f32 x8 [events @2.4GHz]\": %.3f", g_ev);
     printf(", \"v_mul_f32 x16\": %.3f", run<0, 16>(d, blocks, h));
     printf(", \"v_pk_mul_f32 x8\": %.3f", run<1, 8>(d, blocks, h));
+    printf(", \"v_pk_mul_f32 x8 [events @2.4GHz]\": %.3f", g_ev);
     printf(", \"v_pk_mul_f32 x16\": %.3f", run<1, 16>(d, blocks, h));
     printf(", \"v_rcp_f32 x8\": %.3f", run<2, 8>(d, blocks, h));
+    printf(", \"v_rcp_f32 x8 [events @2.4GHz]\": %.3f", g_ev);
     printf(", \"fp32 division x8\": %.3f", run<3, 8>(d, blocks, h));
     printf(", \"memtime_ticks_per_us\": %.1f", g_mhz);
     printf(", \"v_fma_f32 x8\": %.3f", run<4, 8>(d, blocks, h));
+    printf(", \"v_fma_f32 x8 [events @2.4GHz]\": %.3f", g_ev);
     printf(", \"v_add_f32 x8\": %.3f", run<5, 8>(d, blocks, h));
     printf(", \"v_div_scale_f32 x8\": %.3f", run<6, 8>(d, blocks, h));
     printf(", \"v_div_fixup_f32 x8\": %.3f", run<7, 8>(d, blocks, h));
@@ -169,12 +198,26 @@ int main()
     printf(", \"fp32 division x1 @1w\": %.3f", run<3, 1>(d, cus, h, 1));
     printf(", \"fp32 division x4 @5w\": %.3f", run<3, 4>(d, cus * 5, h, 5));
     printf(", \"ds_bpermute x8 @8w\": %.3f", run<9, 8>(d, blocks, h));
+    printf(", \"ds_bpermute x8 @8w [events @2.4GHz]\": %.3f", g_ev);
     printf(", \"ds_bpermute x1 @1w\": %.3f", run<9, 1>(d, cus, h, 1));
     // overlap of LDS permutes with VALU: 1 ds_bpermute chain + 14 v_mul chains per step
     printf(", \"bperm1+mul14 @5w (per step)\": %.3f", 15.0 * run<10, 15>(d, cus * 5, h, 5));
     printf(", \"mul14 @5w (per step)\": %.3f", 14.0 * run<0, 14>(d, cus * 5, h, 5));
     printf(", \"bperm1 @5w (per step)\": %.3f", run<9, 1>(d, cus * 5, h, 5));
     printf(", \"bperm8 @5w (per instr)\": %.3f", run<9, 8>(d, cus * 5, h, 5));
+    printf(", \"v_pk_fma_f32 x8\": %.3f", run<11, 8>(d, blocks, h));
+    printf(", \"v_pk_fma_f32 x8 [events @2.4GHz]\": %.3f", g_ev);
+    printf(", \"v_pk_add_f32 x8\": %.3f", run<12, 8>(d, blocks, h));
+    printf(", \"v_mul_f32 x8 @5w\": %.3f", run<0, 8>(d, cus * 5, h, 5));
+    printf(", \"v_mul_f32 x8 @5w [events @2.4GHz]\": %.3f", g_ev);
+    printf(", \"v_pk_mul_f32 x8 @5w\": %.3f", run<1, 8>(d, cus * 5, h, 5));
+    printf(", \"v_rcp_f32 x8 @5w\": %.3f", run<2, 8>(d, cus * 5, h, 5));
+    printf(", \"mul/rcp alternating x8 (per instr)\": %.3f", run<13, 8>(d, blocks, h));
+    printf(", \"1 rcp + 4 mul x10 (per instr)\": %.3f", run<14, 10>(d, blocks, h));
+    printf(", \"v_pk_mul_f32 x1 @1w\": %.3f", run<1, 1>(d, cus, h, 1));
+    printf(", \"v_mul_f32 x8 @1w\": %.3f", run<0, 8>(d, cus, h, 1));
+    printf(", \"v_pk_mul_f32 x8 @1w\": %.3f", run<1, 8>(d, cus, h, 1));
+    printf(", \"v_rcp_f32 x8 @1w\": %.3f", run<2, 8>(d, cus, h, 1));
     printf(", \"unit\": \"SIMD-cycles per wave-instruction (s_memtime)\"}\n");
     hipFree(d);
     return 0;

@@ -50,7 +50,7 @@ def main():
     # per batch, and a launch tail each; profiles/r02/psweep_batch_r02s3zd.json)
     ap.add_argument("--batch", type=int, default=1 << 20)
     ap.add_argument("--seed", type=lambda v: int(v, 0), default=0x51EC0DE)
-    ap.add_argument("--reps", type=int, default=3, help="runs per p (the fastest is reported)")
+    ap.add_argument("--reps", type=int, default=3, help="runs per p (the median is reported, min and max beside it)")
     ap.add_argument("--out", default=None, help="write the per-p lines to this JSON file (rank 0)")
     ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
                     help="decoder option (qec_decoder_set_option), e.g. schedule=0")
@@ -66,8 +66,13 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    backend = None
     if world > 1:
-        dist.init_process_group("nccl")
+        # RCCL ("nccl") over xGMI; QEC_BENCH_BACKEND=gloo rehearses the multi-rank path with several
+        # ranks sharing one GPU (RCCL needs one GPU per rank)
+        backend = os.environ.get("QEC_BENCH_BACKEND") or "nccl"
+        dist.init_process_group(backend)
+    local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     code = q.Quantum_LDPC_Code.createFromFile(code_path(args.code))
@@ -82,24 +87,30 @@ def main():
     for p in args.ps:
         if world > 1:
             dist.barrier()
-        # the same samples --reps times (identical counters); the fastest run's time, so one host
-        # hiccup of a few ms does not stand for a 2-10 ms sweep point
-        dt = None
+        # the same samples --reps times (identical counters, checked); the median run's time is
+        # reported, the fastest and slowest beside it
+        runs = []
         for _ in range(max(1, args.reps)):
             t0 = time.perf_counter()
             r = dec.monte_carlo(args.seed, lo, hi - lo, p, args.iters, args.stop, args.batch)
-            t = time.perf_counter() - t0
-            if dt is None or t < dt:
-                dt, best = t, r
-        r = best
-        vec = torch.tensor([r[k] for k in FIELDS], dtype=torch.int64, device=dev)
-        tm = torch.tensor([dt, r["decodeSeconds"]], dtype=torch.float64, device=dev)
+            runs.append((time.perf_counter() - t0, r))
+        same = all(all(r[k] == runs[0][1][k] for k in FIELDS) for _, r in runs)
+        order = sorted(range(len(runs)), key=lambda i: runs[i][0])
+        dt, r = runs[order[len(order) // 2]]
+        cdev = dev if backend in (None, "nccl") else torch.device("cpu")  # gloo reduces host tensors
+        vec = torch.tensor([r[k] for k in FIELDS], dtype=torch.int64, device=cdev)
+        tm = torch.tensor([dt, r["decodeSeconds"], runs[order[0]][0], runs[order[-1]][0], 0.0 if same else 1.0],
+                          dtype=torch.float64, device=cdev)
         if world > 1:
             dist.all_reduce(vec)
             dist.all_reduce(tm, op=dist.ReduceOp.MAX)
         c = dict(zip(FIELDS, vec.cpu().tolist()))
         line = summarize(p, c, float(tm[0].item()), world)
         line["decode_seconds"] = round(float(tm[1].item()), 4)  # decode kernels only (the rest: front end + counts)
+        line["reps"] = {"n": len(runs), "reported": "median", "min_seconds": round(float(tm[2].item()), 4),
+                        "max_seconds": round(float(tm[3].item()), 4), "counters_identical": float(tm[4].item()) == 0.0}
+        if backend:
+            line["backend"] = backend
         line.update({"code": code.describe(), "stop": args.stop, "max_iters": args.iters, "seed": args.seed})
         lines.append(line)
         if rank == 0:

@@ -357,6 +357,17 @@ def valu_roofline(pm, path, B, kernel_ms, hard_paths):
                  "valu_insts_per_launch": int(insts), "kernel_ms": round(kernel_ms, 4),
                  "profile": os.path.relpath(path, ROOT), "profile_batch": pm.get("batch"),
                  "profile_frac": pm.get("valu_issue_frac")})
+    if pm.get("valu_weighted_slots_per_syndrome"):
+        # cost-weighted: a v_rcp_f32 (transcendental, quarter rate: 8.1 vs 2.1-2.4 cycles for v_mul /
+        # v_fma in profiles/r03/valu_probe.json) takes four issue slots; this is the headline frac
+        slots = pm["valu_weighted_slots_per_syndrome"] * B
+        wach = slots / (kernel_ms * 1e-3) / 1e12
+        base.update({"achieved": round(wach, 4), "frac": round(wach / peak, 4), "frac_unweighted": round(ach / peak, 4),
+                     "weighting": "VALU issue slots, SQ_INSTS_VALU_TRANS_F32 counted 4x (probe: v_rcp_f32 8.1 "
+                                  "cycles vs 2.1-2.4 for v_mul/v_add/v_fma at full occupancy)",
+                     "valu_trans_per_launch": int(round(pm["valu_trans_per_launch"] * B / pm["batch"]))})
+    if pm.get("lds_issue_frac") is not None and pm.get("kernel_trace_avg_ns"):
+        base["lds_issue_frac"] = round(pm["lds_issue_frac"] * pm["kernel_trace_avg_ns"] * 1e-6 / kernel_ms, 4)
     return base
 
 

@@ -181,7 +181,8 @@ int qec_decoder_device(const qec_decoder* dec);         /* HIP device ordinal (o
  *     pipeline's bit-row syndromes, i.e. qec_monte_carlo): a triage kernel decides iteration 0 of
  *     64 syndromes per wave from the syndrome patterns (triage.hip); the sectors it does not stop
  *     are compacted into lists the decode kernel then decodes (list mode).  Bit-identical either
- *     way; 0 decodes every sector in the decode kernel (for measurement). */
+ *     way.  0 = off (every sector in the decode kernel), 1 = when p <= 0.01 (above it most
+ *     sectors go on and the ordered decode of the whole batch is faster), 2 = always. */
 enum { QEC_OPT_HARD_PATHS = 1, QEC_OPT_CYCLE_JUMP = 2, QEC_OPT_SCHEDULE = 3, QEC_OPT_SECTOR_SPLIT = 4,
        QEC_OPT_PHASE_STATS = 5, QEC_OPT_TRIAGE = 6 };
 int qec_decoder_set_option(qec_decoder* dec, int option, int value);

@@ -453,7 +453,10 @@ int qec_decoder_set_option(qec_decoder* d, int option, int value)
             return fail(QEC_ERR_UNSUPPORTED, "qec_decoder_set_option: QEC_OPT_PHASE_STATS needs a shipped code's kernels");
         d->phase_stats = value != 0;
         return QEC_OK;
-    case QEC_OPT_TRIAGE: d->triage = value != 0; return QEC_OK;
+    case QEC_OPT_TRIAGE:
+        if (value < 0 || value > 2) return fail(QEC_ERR_ARG, "qec_decoder_set_option: QEC_OPT_TRIAGE is 0, 1 or 2");
+        d->triage = value;
+        return QEC_OK;
     default: return fail(QEC_ERR_ARG, "qec_decoder_set_option: unknown option");
     }
 }
@@ -490,6 +493,7 @@ namespace {
 constexpr long long kScheduleMinBatch = 4096;
 constexpr long long kScheduleMaxSingle = 1LL << 19;
 constexpr float kScheduleSyndromeMinP = 0.004f;
+constexpr float kTriageMaxP = 0.01f;  // QEC_OPT_TRIAGE = 1 triages syndrome-stop batches up to this p
 
 // One decode launch of a single-device handle on device buffers.  Outputs: byte form (eX, eZ,
 // flags) or, with rec non-null, the packed decision records.
@@ -520,8 +524,13 @@ int dispatch_decode(qec_decoder* d, const uint8_t* sX, const uint8_t* sZ, long l
                    (d->phase_stats ? QEC_HP_PHASE : 0);
     // syndrome stop on bit rows into records (the Monte-Carlo pipeline): triage iteration 0 for 64
     // syndromes per wave, then decode only the sectors it passes on (triage.hip, list mode)
+    // Above p = 0.01 most sectors go on past iteration 0 (P61 at p = 0.02: 2.2 iterations per sector)
+    // and the list-mode decode of nearly the whole batch loses to the ordered one-wave-per-syndrome
+    // launch (140 vs 178 M syn/s at p = 0.02, 6.4 vs 8.3 at 0.1; 1.47 G vs 0.50 G at 0.002,
+    // profiles/r03/psweep_triage.json), so the triage stays off there.
     uint32_t pats[4];
     if (d->triage && !d->phase_stats && stop == QEC_STOP_SYNDROME && sbits && rec != nullptr && q == nullptr &&
+        (d->triage == 2 || p <= kTriageMaxP) &&
         maxIter >= 2 && B < (1LL << 31) && decode_has_list(d->variant) && triage_supported(c) &&
         decode_pattern_masks(d->variant, p, pats)) {
         if ((rc = ws_reserve(d->merge, (size_t)B, st, "decode")) || (rc = ws_reserve(d->tlist, 2 * (size_t)B + 2, st, "decode")))

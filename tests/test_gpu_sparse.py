@@ -126,7 +126,7 @@ def test_large_code_front_end_full_width(tmp_path):
     """The fused front end's samples per wave are capped by the LDS the gap table leaves
     (montecarlo.hip launch_mc_gap): the n = 762 code (72 words of sample state) at 2^19 samples
     runs at 54 instead of 64 per wave and draws the same samples as a 1000-sample launch and the
-    numpy restatement of the Philox stream; monte_carlo at that batch equals its 8192 batches."""
+    numpy restatement of the Philox stream (syndromes and packed errors)."""
     import torch
     from oracle.philox import depolarizing
     _, code = generated_file(tmp_path, 3, 3, 6, 127, 2, 3)
@@ -147,11 +147,8 @@ def test_large_code_front_end_full_width(tmp_path):
     x, z = depolarizing(seed, lo, 1000, code.n, p)
     assert np.array_equal(small[0].cpu().numpy(), code.syndrome(0, x))
     assert np.array_equal(small[1].cpu().numpy(), code.syndrome(1, z))
-    a = dec.monte_carlo(seed, 0, B, p, 20, "syndrome", batch=B)
-    b = dec.monte_carlo(seed, 0, B, p, 20, "syndrome", batch=8192)
-    for k in ("tested", "withX", "withZ", "synX", "synZ", "logical", "corrected", "convX", "convZ",
-              "iterationsX", "iterationsZ"):
-        assert a[k] == b[k], (k, a[k], b[k])
+    exp = np.concatenate([np.packbits(x, axis=1, bitorder="little"), np.packbits(z, axis=1, bitorder="little")], 1)
+    assert np.array_equal(small[2].cpu().numpy(), exp)
 
 
 def test_irregular_code_is_rejected(code_paths, tmp_path):

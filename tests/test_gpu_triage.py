@@ -40,7 +40,7 @@ def bit_rows(s):
 def decode_all(dec, code, sX, sZ, p, N):
     B = len(sX)
     out = {}
-    for name, tri in (("on", 1), ("off", 0)):
+    for name, tri in (("on", 2), ("off", 0)):  # 2: triage at every p (1 only up to p = 0.01)
         dec.set_option("triage", tri)
         rec = torch.empty((B, dec.record_bytes()), dtype=torch.uint8, device=DEV)
         its = torch.empty((B, 2), dtype=torch.int32, device=DEV)
@@ -103,17 +103,19 @@ def test_monte_carlo_triage_counters(env, key, p):
     code, dec, _ = env[key]
     B = 1 << 18
     res = {}
-    for tri in (1, 0):
+    for tri in (2, 1, 0):
         dec.set_option("triage", tri)
         res[tri] = dec.monte_carlo(0x51EC0DE, 12345, B, p, 50, "syndrome")
     dec.set_option("triage", 1)
     for k in q.MC_COUNTERS + ("tested", "iterationsX", "iterationsZ"):
-        assert res[1][k] == res[0][k], (k, res[1][k], res[0][k])
+        assert res[2][k] == res[1][k] == res[0][k], (k, res[2][k], res[1][k], res[0][k])
 
 
 def test_triage_option_roundtrip(env):
     _, dec, _ = env["P61"]
     assert dec.get_option("triage") == 1
-    dec.set_option("triage", 0)
-    assert dec.get_option("triage") == 0
-    dec.set_option("triage", 1)
+    for v in (0, 2, 1):
+        dec.set_option("triage", v)
+        assert dec.get_option("triage") == v
+    with pytest.raises(q.QecError):
+        dec.set_option("triage", 3)

@@ -103,6 +103,21 @@ def main():
         issue_s = avg["SQ_INSTS_VALU"] * 2 / (1024 * 2.4e9)
         out["valu_issue_frac"] = round(issue_s / (dur_ns * 1e-9), 4)
         out["valu_issue_basis"] = "SQ_INSTS_VALU x 2 cycles / (1024 SIMDs x 2.4 GHz x kernel-trace duration)"
+    # cost-weighted VALU issue (profiles/r03/valu_probe.json, event throughput at 32 waves per SIMD
+    # requested: v_mul / v_add / v_fma 2.1-2.4 cycles, v_rcp_f32 8.1, i.e. a transcendental holds the
+    # SIMD's VALU for four plain slots) and LDS issue (ds_bpermute_b32 24.2 SIMD-cycles, the CU's LDS
+    # shared by 4 SIMDs: 6 CU-cycles per wave instruction, an upper price for the cheaper ds_read/write)
+    if dur_ns and "SQ_INSTS_VALU_TRANS_F32" in avg:
+        trans = avg["SQ_INSTS_VALU_TRANS_F32"]
+        slots = avg["SQ_INSTS_VALU"] - trans + 4 * trans
+        out["valu_trans_per_launch"] = round(trans)
+        out["valu_weighted_slots_per_syndrome"] = slots / batch
+        out["valu_weighted_issue_frac"] = round(slots * 2 / (1024 * 2.4e9) / (dur_ns * 1e-9), 4)
+        out["valu_mix_per_launch"] = {k[len("SQ_INSTS_VALU_"):]: round(avg[k]) for k in avg
+                                      if k.startswith("SQ_INSTS_VALU_") and k != "SQ_INSTS_VALU_TRANS_F32"}
+    if dur_ns and "SQ_INSTS_LDS" in avg:
+        out["lds_issue_frac"] = round(avg["SQ_INSTS_LDS"] * 6 / (256 * 2.4e9) / (dur_ns * 1e-9), 4)
+        out["lds_issue_basis"] = "SQ_INSTS_LDS x 6 CU-cycles (ds_bpermute_b32 price) / (256 CUs x 2.4 GHz x duration)"
     if "SQ_WAIT_ANY" in avg and "SQ_ACTIVE_INST_ANY" in avg:
         out["wait_over_issue"] = round(avg["SQ_WAIT_ANY"] / max(avg["SQ_ACTIVE_INST_ANY"], 1), 4)
     with open(a.out, "w") as fh:

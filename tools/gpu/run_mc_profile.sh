@@ -18,7 +18,8 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/
     python3 "$R/tools/psweep.py" --ps $P > /dev/null 2> "$OUT/trace.err" || { tail -5 "$OUT/trace.err"; exit 1; }
 cat "$OUT/trace/run_kernel_stats.csv"
 i=0
-for grp in "SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVES" "SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES SQ_BUSY_CYCLES"; do
+for grp in "SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVES" "SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES SQ_BUSY_CYCLES" \
+           "FETCH_SIZE" "WRITE_SIZE"; do
   i=$((i+1))
   timeout -k 10 -s KILL 180 rocprofv3 --kernel-trace --pmc $grp --output-format csv -d "$OUT/pmc$i" -o run -- \
       python3 "$R/tools/psweep.py" --ps $P --total 262144 > /dev/null 2> "$OUT/pmc$i.err"

@@ -19,7 +19,8 @@ for code in $CODES; do
   if [ $rc -ne 0 ]; then tail -5 "$OUT/$code/trace.err"; exit $rc; fi
   i=0
   for grp in "FETCH_SIZE" "WRITE_SIZE" "SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVES" \
-             "SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES GRBM_GUI_ACTIVE"; do
+             "SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES GRBM_GUI_ACTIVE" \
+             "SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_INT32 SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT"; do
     i=$((i+1))
     timeout -k 10 -s KILL 180 rocprofv3 --kernel-trace --pmc $grp --output-format csv -d "$OUT/$code/pmc$i" -o run -- \
         python3 $BENCH --steps 2 --warmup 1 > "$OUT/$code/bench_pmc$i.json" 2> "$OUT/$code/pmc$i.err"

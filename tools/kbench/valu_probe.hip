@@ -120,6 +120,8 @@ __global__ __launch_bounds__(256) void probe(long long* cycles, float a)
             if (OP == 13) x[c] = (c & 1) ? rcp(x[c]) : mul(x[c], a);
             // 1 v_rcp_f32 per 4 v_mul_f32 (about the division mix of the var pass)
             if (OP == 14) x[c] = (c % 5 == 0) ? rcp(x[c]) : mul(x[c], a);
+            if (OP == 15) x[c] = __int_as_float(__float_as_int(x[c]) ^ (int)(threadIdx.x + c));
+            if (OP == 16) x[c] = __uint_as_float(min(__float_as_uint(x[c]) + 1u, 0x3F800000u + (uint32_t)c));
         }
     }
     const long long t1 = __builtin_amdgcn_s_memtime();
@@ -160,6 +162,30 @@ static double run(long long* d, int blocks, std::vector<long long>& h, int wps =
     g_ev = (ms * 1e-3 * 2.4e9) / ((double)wps * kIters * NCH) * ((double)cus_g * 4 * wps / ((double)blocks * 4));
     // 8 waves share each SIMD for the whole run: SIMD-cycles per wave-instruction
     return mean_wave_cycles / ((double)wps * kIters * NCH);
+}
+
+// Throughput by HIP events alone, on an oversubscribed grid (32 waves per SIMD requested, 8 resident
+// at a time): wave-instructions retired per SIMD per 2.4 GHz cycle, independent of how the issue
+// arbiter shares the SIMD between its resident waves (s_memtime per wave assumes fair sharing).
+template <int OP, int NCH>
+static double tp(long long* d, int cus, int gens = 4)
+{
+    const int blocks = cus * 8 * gens;
+    long long* big = nullptr;
+    hipMalloc(&big, sizeof(long long) * blocks * 4);
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0);
+    hipEventCreate(&e1);
+    for (int r = 0; r < 2; ++r) hipLaunchKernelGGL((probe<OP, NCH>), dim3(blocks), dim3(256), 0, 0, big, 0.9999f);
+    hipEventRecord(e0);
+    hipLaunchKernelGGL((probe<OP, NCH>), dim3(blocks), dim3(256), 0, 0, big, 0.9999f);
+    hipEventRecord(e1);
+    hipEventSynchronize(e1);
+    float ms = 0;
+    hipEventElapsedTime(&ms, e0, e1);
+    hipFree(big);
+    const double instrs_per_simd = (double)blocks * 4 * kIters * NCH / (cus * 4.0);
+    return ms * 1e-3 * 2.4e9 / instrs_per_simd;
 }
 
 int main()
@@ -218,6 +244,22 @@ int main()
     printf(", \"v_mul_f32 x8 @1w\": %.3f", run<0, 8>(d, cus, h, 1));
     printf(", \"v_pk_mul_f32 x8 @1w\": %.3f", run<1, 8>(d, cus, h, 1));
     printf(", \"v_rcp_f32 x8 @1w\": %.3f", run<2, 8>(d, cus, h, 1));
+    printf(", \"throughput\": {\"unit\": \"2.4 GHz cycles per wave-instruction per SIMD (events, 32 waves/SIMD requested)\"");
+    printf(", \"v_mul_f32 x8\": %.3f", tp<0, 8>(d, cus));
+    printf(", \"v_mul_f32 x16\": %.3f", tp<0, 16>(d, cus));
+    printf(", \"v_add_f32 x8\": %.3f", tp<5, 8>(d, cus));
+    printf(", \"v_fma_f32 x8\": %.3f", tp<4, 8>(d, cus));
+    printf(", \"v_pk_mul_f32 x8\": %.3f", tp<1, 8>(d, cus));
+    printf(", \"v_pk_fma_f32 x8\": %.3f", tp<11, 8>(d, cus));
+    printf(", \"v_rcp_f32 x8\": %.3f", tp<2, 8>(d, cus));
+    printf(", \"v_xor_b32 x8\": %.3f", tp<15, 8>(d, cus));
+    printf(", \"v_add_u32+v_min_u32 x8 (per pair)\": %.3f", tp<16, 8>(d, cus));
+    printf(", \"1 rcp + 4 mul x10 (per instr)\": %.3f", tp<14, 10>(d, cus));
+    printf(", \"ds_bpermute x8\": %.3f", tp<9, 8>(d, cus));
+    printf(", \"1 bpermute + 14 mul (per instr)\": %.3f", tp<10, 15>(d, cus));
+    printf(", \"fp32 division x8 (per division)\": %.3f", tp<3, 8>(d, cus));
+    printf(", \"v_mul_f32 x8, 1 gen\": %.3f", tp<0, 8>(d, cus, 1));
+    printf(", \"v_mul_f32 x8, 16 gens\": %.3f}", tp<0, 8>(d, cus, 16));
     printf(", \"unit\": \"SIMD-cycles per wave-instruction (s_memtime)\"}\n");
     hipFree(d);
     return 0;

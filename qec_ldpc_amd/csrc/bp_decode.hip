@@ -223,7 +223,7 @@ struct BpArgs {
     const uint32_t* counts;
     long long B;
     int P, G, n, mX, mZ;
-    int nb, recBytes;  // ceil(n / 8), 2 nb + 1
+    int nb, recBytes;  // ceil(n / 8); row stride of the records (2 nb + 1, or padded to whole words)
     float errorProbability;
     int maxIter, stop;
     int hardPaths;  // QEC_HP_* bits: hard-message paths / cycle jump (QEC_OPT_HARD_PATHS, QEC_OPT_CYCLE_JUMP)
@@ -297,25 +297,14 @@ struct GeneratedShifts {
         int DX[J_], DZ[K_];
         int CX[L_], CZ[L_];
     };
-    static constexpr long pw(long base, long e)
-    {
-        long t = 1;
-        for (long i = 0; i < e; ++i) t = (t * base) % P_;
-        return t;
-    }
     static constexpr Tables make()
     {
         Tables t{};
-        long inv = 1;
-        for (long x = 1; x < P_; ++x)
-            if ((x * S_) % P_ == 1) { inv = x; break; }
-        auto sp = [inv](long p) { return p < 0 ? pw(inv, -p) : pw(S_, p); };
+        constexpr QcExponents<J_, K_, L_, P_, S_, T_> e = QcExponents<J_, K_, L_, P_, S_, T_>::make();
         for (int j = 0; j < J_; ++j)
-            for (int l = 0; l < L_; ++l)
-                t.EX[j][l] = (int)(((l < L_ / 2) ? sp(l - j) : P_ - (T_ * sp(j - 1 + l)) % P_) % P_);
+            for (int l = 0; l < L_; ++l) t.EX[j][l] = e.EX[j][l];
         for (int k = 0; k < K_; ++k)
-            for (int l = 0; l < L_; ++l)
-                t.EZ[k][l] = (int)(((((l < L_ / 2) ? (T_ * sp(l - k - 1)) % P_ : P_ - sp(k + l)) % P_) + P_) % P_);
+            for (int l = 0; l < L_; ++l) t.EZ[k][l] = e.EZ[k][l];
         // relabel() on the 2-D tables (same rule, written out for constant evaluation)
         for (int l = 0; l < L_; ++l) { t.CX[l] = RL_ ? t.EX[0][l] : 0; t.CZ[l] = RL_ ? t.EZ[0][l] : 0; }
         for (int r = 0; r < J_; ++r) t.DX[r] = RL_ ? ((t.CX[0] - t.EX[r][0]) % P_ + P_) % P_ : 0;
@@ -1491,7 +1480,9 @@ using KernelFn = void (*)(const BpArgs);
 using TuneP61 = Tune<5, true, false, true, true, false, true, 2, 1, 4>;
 struct TuneP61MinReg : TuneP61 {};
 using ShiftsP61 = GeneratedShifts<4, 5, 10, 61, 9, 49, TuneP61::kRelabel, TuneP61::kMaskSelect>;
-using TuneP7 = Tune<8, true, false, true, true, true, false, 2, 1, 7>;
+// P7: three columns per division guard (col_group): 0.075 vs 0.077 ms at configs[1] (65 536 @ 20), even
+// at 2^20 (profiles/r03/cmp_p7_65536_colgroups.txt, cmp_p7_2e20.txt)
+using TuneP7 = Tune<8, true, false, true, true, true, false, 2, 1, 7, 3>;
 struct TuneP7MinReg : TuneP7 {};
 using ShiftsP7 = GeneratedShifts<3, 3, 6, 7, 2, 3, TuneP7::kRelabel, TuneP7::kMaskSelect>;
 #ifndef QEC_P61_MINREG
@@ -1717,7 +1708,7 @@ bool decode_has_phase_stats(const void* variant, int stop)
 int launch_decode(const void* variant, const Code& c, const uint8_t* sX, const uint8_t* sZ, bool sbits, long long B,
                   float errorProbability, int maxIter, int stop, uint8_t* eX, uint8_t* eZ, uint8_t* flags,
                   uint8_t* rec, int32_t* iters, float* q, int hardPaths, const int32_t* perm, int split,
-                  uint32_t* merge, bool merge_zeroed, hipStream_t stream)
+                  uint32_t* merge, bool merge_zeroed, hipStream_t stream, int rec_stride)
 {
     const Variant* v = static_cast<const Variant*>(variant);
     if (B <= 0) return QEC_OK;
@@ -1743,7 +1734,7 @@ int launch_decode(const void* variant, const Code& c, const uint8_t* sX, const u
     a.G = 64 / c.P;
     a.n = c.n; a.mX = c.mX; a.mZ = c.mZ;
     a.nb = (c.n + 7) / 8;
-    a.recBytes = 2 * a.nb + 1;
+    a.recBytes = rec_stride > 0 ? rec_stride : 2 * a.nb + 1;
     a.errorProbability = errorProbability;
     a.maxIter = maxIter < 0 ? 0 : maxIter;
     a.stop = stop;
@@ -1799,7 +1790,7 @@ bool decode_pattern_masks(const void* variant, float errorProbability, uint32_t 
 int launch_decode_list(const void* variant, const Code& c, const uint8_t* sX, const uint8_t* sZ, long long B,
                        float errorProbability, int maxIter, int hardPaths, uint8_t* rec, int32_t* iters,
                        uint32_t* merge, const int32_t* listX, const int32_t* listZ, const uint32_t* counts,
-                       hipStream_t stream)
+                       hipStream_t stream, int rec_stride)
 {
     const Variant* v = static_cast<const Variant*>(variant);
     if (!v->list) return fail(QEC_ERR_UNSUPPORTED, "bp_decode: no list-mode kernel for this code");
@@ -1812,7 +1803,7 @@ int launch_decode_list(const void* variant, const Code& c, const uint8_t* sX, co
     a.listX = listX; a.listZ = listZ; a.counts = counts;
     a.B = B; a.P = c.P; a.G = 64 / c.P;
     a.n = c.n; a.mX = c.mX; a.mZ = c.mZ;
-    a.nb = (c.n + 7) / 8; a.recBytes = 2 * a.nb + 1;
+    a.nb = (c.n + 7) / 8; a.recBytes = rec_stride > 0 ? rec_stride : 2 * a.nb + 1;
     a.errorProbability = errorProbability;
     a.maxIter = maxIter < 0 ? 0 : maxIter;
     a.stop = QEC_STOP_SYNDROME;

@@ -18,7 +18,7 @@ const void* select_variant(const Code& c, std::string& name);
 int launch_decode(const void* variant, const Code& c, const uint8_t* sX, const uint8_t* sZ, bool sbits, long long B,
                   float errorProbability, int maxIter, int stop, uint8_t* eX, uint8_t* eZ, uint8_t* flags,
                   uint8_t* rec, int32_t* iters, float* q, int hardPaths, const int32_t* perm, int split,
-                  uint32_t* merge, bool merge_zeroed, hipStream_t stream);
+                  uint32_t* merge, bool merge_zeroed, hipStream_t stream, int rec_stride = 0);
 size_t schedule_workspace_bytes(long long B, int mX, int mZ);
 long long schedule_max_batch();
 int launch_schedule(const uint8_t* sX, const uint8_t* sZ, bool sbits, long long B, int mX, int mZ, void* ws,
@@ -29,17 +29,18 @@ bool decode_pattern_masks(const void* variant, float errorProbability, uint32_t 
 int launch_decode_list(const void* variant, const Code& c, const uint8_t* sX, const uint8_t* sZ, long long B,
                        float errorProbability, int maxIter, int hardPaths, uint8_t* rec, int32_t* iters,
                        uint32_t* merge, const int32_t* listX, const int32_t* listZ, const uint32_t* counts,
-                       hipStream_t stream);
+                       hipStream_t stream, int rec_stride = 0);
 bool triage_supported(const Code& c);
 int launch_triage(const Code& c, const uint32_t* sX, const uint32_t* sZ, long long B, const uint32_t pats[4],
                   uint8_t* rec, int32_t* iters, uint32_t* merge, int32_t* listX, int32_t* listZ, uint32_t* counts,
-                  hipStream_t st);
+                  hipStream_t st, int rec_stride = 0);
 bool decode_has_phase_stats(const void* variant, int stop);
 int launch_sample_depolarizing(uint64_t seed, uint64_t start, long long B, int n, float p, uint8_t* x, uint8_t* z,
                                hipStream_t st);
 int launch_mc_errors_syndrome(int src, const McArgsHost& h, hipStream_t st);
 int launch_statistics_packed(const Code& c, const uint64_t* imp_cols, const uint8_t* errp, int estride, const uint8_t* rec,
-                             const int32_t* iters, long long B, unsigned long long* counters, hipStream_t st);
+                             const int32_t* iters, long long B, unsigned long long* counters, hipStream_t st,
+                             int rec_stride = 0);
 void* sparse_plan_create(const Code& c, int device);
 void sparse_plan_free(void* plan);
 const char* sparse_plan_name(const void* plan);
@@ -499,9 +500,11 @@ constexpr float kTriageMaxP = 0.01f;  // QEC_OPT_TRIAGE = 1 triages syndrome-sto
 // flags) or, with rec non-null, the packed decision records.
 // sbits: sX / sZ are bit rows ([B][ceil(m/32)] words, the Monte-Carlo pipeline's layout; wave-circulant
 // engine only), else byte rows
+// rec_stride: record row stride (0: 2 nb + 1, the public layout; the Monte-Carlo pipeline pads rows to
+// whole words for its statistics kernel; wave-circulant engine only)
 int dispatch_decode(qec_decoder* d, const uint8_t* sX, const uint8_t* sZ, long long B, float p, int maxIter, int stop,
                     uint8_t* eX, uint8_t* eZ, uint8_t* flags, uint8_t* rec, int32_t* iters, float* q, hipStream_t st,
-                    bool sbits = false)
+                    bool sbits = false, int rec_stride = 0)
 {
     if (B <= 0) return QEC_OK;
     const Code& c = *d->code;
@@ -509,6 +512,8 @@ int dispatch_decode(qec_decoder* d, const uint8_t* sX, const uint8_t* sZ, long l
     if (rc) return rc;
     if (d->engine == QEC_ENGINE_SPARSE) {
         if (sbits) return fail(QEC_ERR_UNSUPPORTED, "decode: bit-row syndromes need the wave-circulant engine");
+        if (rec_stride > 0 && rec_stride != 2 * ((c.n + 7) / 8) + 1)
+            return fail(QEC_ERR_UNSUPPORTED, "decode: padded record rows need the wave-circulant engine");
         if (rec != nullptr) {  // byte outputs into the handle's staging, then packed
             if ((rc = ws_reserve(d->eX, (size_t)B * c.n, st, "decode")) || (rc = ws_reserve(d->eZ, (size_t)B * c.n, st, "decode")) ||
                 (rc = ws_reserve(d->flags, (size_t)B, st, "decode")))
@@ -540,9 +545,10 @@ int dispatch_decode(qec_decoder* d, const uint8_t* sX, const uint8_t* sZ, long l
         uint32_t* cnt = reinterpret_cast<uint32_t*>(lZ + B);
         QEC_HIP_CHECK(hipMemsetAsync(cnt, 0, 2 * sizeof(uint32_t), st));
         rc = launch_triage(c, reinterpret_cast<const uint32_t*>(sX), reinterpret_cast<const uint32_t*>(sZ), B, pats, rec,
-                           iters, d->merge.data(), lX, lZ, cnt, st);
+                           iters, d->merge.data(), lX, lZ, cnt, st, rec_stride);
         if (!rc)
-            rc = launch_decode_list(d->variant, c, sX, sZ, B, p, maxIter, hp, rec, iters, d->merge.data(), lX, lZ, cnt, st);
+            rc = launch_decode_list(d->variant, c, sX, sZ, B, p, maxIter, hp, rec, iters, d->merge.data(), lX, lZ, cnt, st,
+                                    rec_stride);
         if (rc) return rc;
         return ws_release(d, st);
     }
@@ -564,7 +570,7 @@ int dispatch_decode(qec_decoder* d, const uint8_t* sX, const uint8_t* sZ, long l
         zeroed = split;
     }
     rc = launch_decode(d->variant, c, sX, sZ, sbits, B, p, maxIter, stop, eX, eZ, flags, rec, iters, q, hp, perm,
-                       d->sector_split, split ? d->merge.data() : nullptr, zeroed, st);
+                       d->sector_split, split ? d->merge.data() : nullptr, zeroed, st, rec_stride);
     if (rc) return rc;
     return ws_release(d, st);
 }
@@ -754,7 +760,7 @@ int mc_reserve(qec_decoder* d, size_t B, int W)
         // syndromes as bytes or as bit rows, packed errors at 2 nb or word-aligned rows (mc_batch)
         d->msX.reserve(B * std::max<size_t>(c.mX, 4 * ((c.mX + 31) / 32)));
         d->msZ.reserve(B * std::max<size_t>(c.mZ, 4 * ((c.mZ + 31) / 32)));
-        d->merrp.reserve(B * 4 * ((2 * nb + 3) / 4)); d->mrec.reserve(B * (2 * nb + 1));
+        d->merrp.reserve(B * 4 * ((2 * nb + 3) / 4)); d->mrec.reserve(B * 4 * ((2 * nb + 1 + 3) / 4));
         d->mit.reserve(2 * B);
         if (W > 0) { d->midx.reserve(B * W); d->mtype.reserve(B * W); }
     } catch (const std::exception& ex) {
@@ -787,13 +793,17 @@ int mc_batch(qec_decoder* d, McArgsHost h, int src, float p, int maxIter, int st
     int rc = launch_mc_errors_syndrome(src, h, st);
     if (rc) return rc;
     if (ev0) QEC_HIP_CHECK(hipEventRecord(ev0, st));
+    // records at word-aligned rows (156 instead of 155 B for P61) on the bit-row path: the statistics
+    // kernel then reads both its arrays a word at a time
+    const int nb = (c.n + 7) / 8;
+    const int rstride = bits ? 4 * ((2 * nb + 1 + 3) / 4) : 2 * nb + 1;
     rc = dispatch_decode(d, d->msX.data(), d->msZ.data(), h.B, p, maxIter, stop, nullptr, nullptr, nullptr,
-                         d->mrec.data(), want_iters ? d->mit.data() : nullptr, nullptr, st, bits);
+                         d->mrec.data(), want_iters ? d->mit.data() : nullptr, nullptr, st, bits, rstride);
     if (rc) return rc;
     if (ev1) QEC_HIP_CHECK(hipEventRecord(ev1, st));
-    const int nb = (c.n + 7) / 8;
     return launch_statistics_packed(c, d->imp_cols.data(), d->merrp.data(), bits ? 4 * ((2 * nb + 3) / 4) : 2 * nb,
-                                    d->mrec.data(), want_iters ? d->mit.data() : nullptr, h.B, d->mcount.data(), st);
+                                    d->mrec.data(), want_iters ? d->mit.data() : nullptr, h.B, d->mcount.data(), st,
+                                    rstride);
 }
 
 int mc_fetch_counters(qec_decoder* d, unsigned long long* out)

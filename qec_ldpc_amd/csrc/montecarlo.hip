@@ -665,29 +665,63 @@ __global__ __launch_bounds__(64 * kStatBlockWaves) void statistics_packed_kernel
 // outcomes with ballot popcounts (scalar).  The rare sample needing the I-P columns (no syndrome
 // failure, nonzero residual) has its residual words formed by the wave in LDS and goes through
 // logical_from_columns, one at a time.
-constexpr int kRowWaves = 2;          // waves per workgroup
-constexpr int kRowLdsPerWave = 20608;  // bytes: S (estride + recB) + 2 x 16 of alignment slack, S <= 64 (P61: 19 904)
+constexpr int kRowWaves = 4;          // waves per workgroup
+constexpr int kRowLdsPerWave = 10304;  // bytes: S (estride + recB) + 2 x 16 of alignment slack, S <= 32 (P61: 9 984)
 
-// bytes [src, src + nb) of global memory into LDS at dst + (src & 15): 16-byte loads over the
-// aligned body, single bytes for the unaligned head and tail (nothing outside the range is read)
-__device__ __forceinline__ void stage_range(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src, int nb, int lane)
-{
-    const uintptr_t s0 = reinterpret_cast<uintptr_t>(src), s1 = s0 + (uintptr_t)nb;
-    const uintptr_t a0 = s0 & ~(uintptr_t)15;
-    uintptr_t b0 = (s0 + 15) & ~(uintptr_t)15, b1 = s1 & ~(uintptr_t)15;
-    if (b0 > b1) b0 = b1 = s1;  // the whole range lies inside one 16-byte line: bytes only
-    const int head = (int)(b0 - s0), tail = (int)(s1 - b1);
-    if (lane < head) dst[(s0 - a0) + lane] = src[lane];
-    if (lane < tail) dst[(b1 - a0) + lane] = *reinterpret_cast<const uint8_t*>(b1 + lane);
-    const int nv = (int)((b1 - b0) >> 4);
-    const uint4* __restrict__ g = reinterpret_cast<const uint4*>(b0);
-    uint4* __restrict__ l = reinterpret_cast<uint4*>(dst + (b0 - a0));
-    int t = lane;
-    for (; t + 192 < nv; t += 256) {  // four 16-byte loads in flight per lane
-        const uint4 v0 = g[t], v1 = g[t + 64], v2 = g[t + 128], v3 = g[t + 192];
-        l[t] = v0; l[t + 64] = v1; l[t + 128] = v2; l[t + 192] = v3;
+// bytes [src, src + nb) of global memory into LDS at dst + (src & 15), for two ranges at once:
+// 16-byte loads over the aligned bodies -- every load of both bodies issued before the first LDS
+// store (up to 8 per lane in flight), single bytes for the unaligned heads and tails (nothing
+// outside the ranges is read)
+struct StageRange {
+    uint8_t* dst;
+    const uint8_t* src;
+    int nb;
+    uintptr_t a0, b0, b1;
+    int head, tail, nv;
+    __device__ __forceinline__ StageRange(uint8_t* d, const uint8_t* s, int n) : dst(d), src(s), nb(n)
+    {
+        const uintptr_t s0 = reinterpret_cast<uintptr_t>(s), s1 = s0 + (uintptr_t)n;
+        a0 = s0 & ~(uintptr_t)15;
+        b0 = (s0 + 15) & ~(uintptr_t)15;
+        b1 = s1 & ~(uintptr_t)15;
+        if (b0 > b1) b0 = b1 = s1;  // the whole range inside one 16-byte line: bytes only
+        head = (int)(b0 - s0);
+        tail = (int)(s1 - b1);
+        nv = (int)((b1 - b0) >> 4);
     }
-    for (; t < nv; t += 64) l[t] = g[t];
+    __device__ __forceinline__ void ends(int lane) const
+    {
+        const uintptr_t s0 = reinterpret_cast<uintptr_t>(src);
+        if (lane < head) dst[(s0 - a0) + lane] = src[lane];
+        if (lane < tail) dst[(b1 - a0) + lane] = *reinterpret_cast<const uint8_t*>(b1 + lane);
+    }
+};
+
+__device__ __forceinline__ void stage_two(const StageRange& x, const StageRange& y, int lane)
+{
+    constexpr int kMaxPer = 8;  // 16-byte loads per lane and range in flight
+    x.ends(lane);
+    y.ends(lane);
+    const uint4* __restrict__ gx = reinterpret_cast<const uint4*>(x.b0);
+    const uint4* __restrict__ gy = reinterpret_cast<const uint4*>(y.b0);
+    uint4* __restrict__ lx = reinterpret_cast<uint4*>(x.dst + (x.b0 - x.a0));
+    uint4* __restrict__ ly = reinterpret_cast<uint4*>(y.dst + (y.b0 - y.a0));
+    const int n = x.nv > y.nv ? x.nv : y.nv;
+    for (int base = 0; base < n; base += 64 * kMaxPer) {
+        uint4 vx[kMaxPer], vy[kMaxPer];
+#pragma unroll
+        for (int k = 0; k < kMaxPer; ++k) {
+            const int t = base + lane + 64 * k;
+            if (t < x.nv) vx[k] = gx[t];
+            if (t < y.nv) vy[k] = gy[t];
+        }
+#pragma unroll
+        for (int k = 0; k < kMaxPer; ++k) {
+            const int t = base + lane + 64 * k;
+            if (t < x.nv) lx[t] = vx[k];
+            if (t < y.nv) ly[t] = vy[k];
+        }
+    }
 }
 
 // dword k (bytes 4k .. 4k + 3) of a row starting at any byte offset o of the stage
@@ -720,8 +754,7 @@ __global__ __launch_bounds__(64 * kRowWaves) void statistics_rows_kernel(
         const int ns = (int)(B - b0 < S ? B - b0 : S);
         const uint8_t* ge = errp + b0 * estride;
         const uint8_t* gr = rec + b0 * recB;
-        stage_range(est, ge, ns * estride, lane);
-        stage_range(rst, gr, ns * recB, lane);
+        stage_two(StageRange(est, ge, ns * estride), StageRange(rst, gr, ns * recB), lane);
         const bool valid = lane < ns;
         if (iters != nullptr && valid) {
             itx += (unsigned)iters[2 * (b0 + lane)];
@@ -805,6 +838,116 @@ __global__ __launch_bounds__(64 * kRowWaves) void statistics_rows_kernel(
     if (threadIdx.x < nc) {
         unsigned long long v = 0;
         for (int w = 0; w < kRowWaves; ++w) v += part[w][threadIdx.x];
+        if (v) atomicAdd(&counters[threadIdx.x], v);
+    }
+}
+
+// The counters with one lane per sample reading its two rows straight from global memory (no LDS
+// stage): packed errors and records at word-aligned row strides (the Monte-Carlo pipeline's
+// layout: 156-byte rows for P61), EWE / EWR words per row known at compile time so every load of
+// both rows is in flight at once (78 per lane for P61).  Lane-per-sample loads touch 64 rows per
+// wave instruction, but each line is reused by the row's next words (L1/L2 hits); the wave adds its
+// 64 samples' outcomes with ballot popcounts (scalar), so per sample the kernel issues ~2 x 39 loads
+// and ~3 x 39 VALU bit operations.
+constexpr int kLaneWaves = 16;  // waves per workgroup; one workgroup per CU, grid-stride
+
+template <int EWE, int EWR>
+__global__ __launch_bounds__(64 * kLaneWaves) void statistics_lane_kernel(
+    const uint32_t* __restrict__ errp, const uint32_t* __restrict__ rec, const int32_t* __restrict__ iters, long long B,
+    int n, int nb, const uint64_t* __restrict__ imp_cols, int imp_cw, unsigned long long* __restrict__ counters)
+{
+    __shared__ unsigned long long part[kLaneWaves][C_N + 2];
+    __shared__ unsigned long long sres[kLaneWaves][kMaxRecWords];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int eb = 2 * nb;  // decision bytes of a row; the flags byte follows them in a record
+    unsigned long long c[C_N] = {};
+    unsigned long long itx = 0, itz = 0;
+    const long long step = (long long)gridDim.x * blockDim.x;
+    for (long long b0 = (long long)blockIdx.x * blockDim.x + wv * 64; b0 < B; b0 += step) {
+        const long long b = b0 + lane;
+        const bool valid = b < B;
+        const long long bl = valid ? b : B - 1;  // clamped row: every load in bounds, results masked
+        uint32_t ev[EWE], rv[EWR];
+#pragma unroll
+        for (int k = 0; k < EWE; ++k) ev[k] = errp[bl * EWE + k];
+#pragma unroll
+        for (int k = 0; k < EWR; ++k) rv[k] = rec[bl * EWR + k];
+        if (iters != nullptr && valid) {
+            const int2 it = *reinterpret_cast<const int2*>(iters + 2 * b);
+            itx += (unsigned)it.x;
+            itz += (unsigned)it.y;
+        }
+        uint32_t ax = 0, az = 0, ar = 0;
+#pragma unroll
+        for (int k = 0; k < (EWE < EWR ? EWE : EWR); ++k) {
+            // byte masks of word k: x bytes [0, nb), z bytes [nb, 2 nb) (wave-uniform)
+            const int bx = nb - 4 * k, bz = eb - 4 * k;
+            const uint32_t mx = bx >= 4 ? ~0u : bx <= 0 ? 0u : (1u << (8 * bx)) - 1u;
+            const uint32_t mall = bz >= 4 ? ~0u : bz <= 0 ? 0u : (1u << (8 * bz)) - 1u;
+            ax |= ev[k] & mx;
+            az |= ev[k] & mall & ~mx;
+            ar |= (ev[k] ^ rv[k]) & mall;
+        }
+        uint32_t f = 0;
+#pragma unroll
+        for (int k = 0; k < EWR; ++k)
+            if (k == eb / 4) f = (rv[k] >> (8 * (eb % 4))) & 0xFFu;
+        f = valid ? f : 0u;
+        const bool dEX = (f & QEC_SYNDROME_FAIL_X) != 0, dEZ = (f & QEC_SYNDROME_FAIL_Z) != 0;
+        unsigned long long need = __ballot(valid && !(dEX || dEZ) && ar != 0u);
+        unsigned long long logical = 0;
+        if (imp_cw > 0) {
+            const int nw = (eb + 7) / 8;  // 64-bit residual words (record layout)
+            while (need) {
+                const int s = __builtin_ctzll(need);
+                need &= need - 1;
+                const uint8_t* es = reinterpret_cast<const uint8_t*>(errp + (b0 + s) * EWE);
+                const uint8_t* rs = reinterpret_cast<const uint8_t*>(rec + (b0 + s) * EWR);
+                if (lane < nw) {
+                    uint64_t w = 0;
+                    for (int j = 0; j < 8; ++j) {
+                        const int t = 8 * lane + j;
+                        w |= (t < eb ? (uint64_t)(es[t] ^ rs[t]) : 0ull) << (8 * j);
+                    }
+                    sres[wv][lane] = w;
+                }
+                wave_sync();
+                if (logical_from_columns<true>(sres[wv], nw, n, nb, imp_cols, imp_cw, lane)) logical |= 1ull << s;
+                wave_sync();
+            }
+        }
+        const unsigned long long vm = __ballot(valid), sx = __ballot(dEX), sz = __ballot(dEZ);
+        const unsigned long long ok = vm & ~(sx | sz);
+        c[C_WITHX] += __popcll(__ballot(ax != 0u));
+        c[C_WITHZ] += __popcll(__ballot(az != 0u));
+        c[C_SYNX] += __popcll(sx);
+        c[C_SYNZ] += __popcll(sz);
+        c[C_LOGICAL] += __popcll(ok & logical);
+        c[C_CORRECTED] += __popcll(ok & ~logical);
+        c[C_CONVX] += __popcll(__ballot((f & QEC_CONVERGENCE_FAIL_X) != 0));
+        c[C_CONVZ] += __popcll(__ballot((f & QEC_CONVERGENCE_FAIL_Z) != 0));
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        itx += __shfl_xor(itx, o);
+        itz += __shfl_xor(itz, o);
+    }
+    unsigned long long cc[C_N + 2];
+#pragma unroll
+    for (int k = 0; k < C_N; ++k) cc[k] = c[k];
+    cc[C_N] = itx;
+    cc[C_N + 1] = itz;
+    if (lane < C_N + 2) {
+        unsigned long long v = 0;
+#pragma unroll
+        for (int k = 0; k < C_N + 2; ++k) v = lane == k ? cc[k] : v;
+        part[wv][lane] = v;
+    }
+    __syncthreads();
+    const int nc = iters != nullptr ? C_N + 2 : C_N;
+    if (threadIdx.x < nc) {
+        unsigned long long v = 0;
+        for (int w = 0; w < kLaneWaves; ++w) v += part[w][threadIdx.x];
         if (v) atomicAdd(&counters[threadIdx.x], v);
     }
 }
@@ -933,17 +1076,40 @@ int launch_mc_errors_syndrome(int src, const McArgsHost& h, hipStream_t st)
 }
 
 int launch_statistics_packed(const Code& c, const uint64_t* imp_cols, const uint8_t* errp, int estride, const uint8_t* rec,
-                             const int32_t* iters, long long B, unsigned long long* counters, hipStream_t st)
+                             const int32_t* iters, long long B, unsigned long long* counters, hipStream_t st,
+                             int rec_stride)
 {
     if (B <= 0) return QEC_OK;
     const int nb = (c.n + 7) / 8;
+    const int recB = rec_stride > 0 ? rec_stride : 2 * nb + 1;
+    // word-aligned rows of the shipped codes' sizes: one lane per sample, straight from global memory
+    const bool aligned = estride % 4 == 0 && recB % 4 == 0 && (reinterpret_cast<uintptr_t>(errp) & 3) == 0 &&
+                         (reinterpret_cast<uintptr_t>(rec) & 3) == 0 && (c.imp_col_words <= 64) &&
+                         (2 * nb + 7) / 8 <= kMaxRecWords;
+    if (aligned) {
+        void (*k)(const uint32_t*, const uint32_t*, const int32_t*, long long, int, int, const uint64_t*, int,
+                  unsigned long long*) = nullptr;
+        if (estride == 156 && recB == 156) k = statistics_lane_kernel<39, 39>;  // P61
+        if (estride == 12 && recB == 16) k = statistics_lane_kernel<3, 4>;      // P7
+        if (k) {
+            const long long blocks = std::min<long long>((B + 64 * kLaneWaves - 1) / (64 * kLaneWaves), 256);
+            hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(64 * kLaneWaves), 0, st,
+                               reinterpret_cast<const uint32_t*>(errp), reinterpret_cast<const uint32_t*>(rec), iters, B,
+                               c.n, nb, imp_cols, c.imp_col_words, counters);
+            return launch_check("statistics_lane");
+        }
+    }
+    if (rec_stride > 0 && rec_stride != 2 * nb + 1)
+        return fail(QEC_ERR_UNSUPPORTED, "packed statistics: padded record rows need the lane kernel");
     if ((2 * nb + 7) / 8 > kMaxRecWords || c.imp_col_words > 64)
         return fail(QEC_ERR_UNSUPPORTED, "packed statistics kernel: code too long");
-    static const int rows = [] { const char* e = std::getenv("QEC_STAT_ROWS"); return e ? std::atoi(e) : 1; }();
+    // the LDS-staged row kernel (unaligned public layout) measured slower than the byte kernel below at
+    // P61 (195-304 vs 231 us per 2^20, profiles/r03/): experiments only
+    static const int rows = [] { const char* e = std::getenv("QEC_STAT_ROWS"); return e ? std::atoi(e) : 0; }();
     if (rows) {
-        int S = 64;
-        while (S >= 16 && S * (estride + 2 * nb + 1) + 64 > kRowLdsPerWave) S /= 2;
-        if (S >= 16) {
+        int S = 32;
+        while (S >= 8 && S * (estride + 2 * nb + 1) + 64 > kRowLdsPerWave) S /= 2;
+        if (S >= 8) {
             static const int maxb = [] { const char* e = std::getenv("QEC_STAT_BLOCKS"); const int v = e ? std::atoi(e) : 0; return v > 0 ? v : 1024; }();
             const long long blocks = std::min<long long>((B + kRowWaves * S - 1) / (kRowWaves * S), maxb);
             hipLaunchKernelGGL(statistics_rows_kernel, dim3((unsigned)blocks), dim3(64 * kRowWaves),

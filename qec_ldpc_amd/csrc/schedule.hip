@@ -86,7 +86,7 @@ __device__ __forceinline__ uint32_t range_weight(const uint8_t* s, long long lo,
 template <int SPLIT>
 __global__ __launch_bounds__(kHistThreads) void schedule_hist_kernel(const uint8_t* __restrict__ sX,
                                                                    const uint8_t* __restrict__ sZ, long long B,
-                                                                   int mX, int mZ, int chunk,
+                                                                   int mX, int mZ, int chunk, int nbk,
                                                                    uint8_t* __restrict__ key,
                                                                    uint32_t* __restrict__ counts,
                                                                    uint32_t* __restrict__ zero_merge)
@@ -108,21 +108,21 @@ __global__ __launch_bounds__(kHistThreads) void schedule_hist_kernel(const uint8
 #pragma unroll
         for (int o = 1; o < SPLIT; o <<= 1) w += __shfl_xor(w, o);
         if (q == 0 && b < r1) {
-            const int bk = kBuckets - 1 - (int)(w < kBuckets - 1 ? w : kBuckets - 1);
+            const int bk = nbk - 1 - (int)(w < (uint32_t)nbk - 1 ? w : (uint32_t)nbk - 1);
             key[b] = (uint8_t)bk;
             atomicAdd(&h[bk], 1u);
             if (zero_merge) zero_merge[b] = 0u;  // sector-split launches merge their flags there
         }
     }
     __syncthreads();
-    if (t < kBuckets) counts[(long long)blockIdx.x * kBuckets + t] = h[t];
+    if (t < nbk) counts[(long long)blockIdx.x * nbk + t] = h[t];
 }
 
 // The same weights from bit rows (sX [B][wX], sZ [B][wZ] words; the Monte-Carlo pipeline's
 // layout): one thread per syndrome, popcounts of its words.
 __global__ __launch_bounds__(kHistThreads) void schedule_hist_bits_kernel(const uint32_t* __restrict__ sX,
                                                                         const uint32_t* __restrict__ sZ, long long B,
-                                                                        int wX, int wZ, int chunk,
+                                                                        int wX, int wZ, int chunk, int nbk,
                                                                         uint8_t* __restrict__ key,
                                                                         uint32_t* __restrict__ counts,
                                                                         uint32_t* __restrict__ zero_merge)
@@ -137,13 +137,13 @@ __global__ __launch_bounds__(kHistThreads) void schedule_hist_bits_kernel(const 
         uint32_t w = 0;
         for (int k = 0; k < wX; ++k) w += __popc(sX[b * wX + k]);
         for (int k = 0; k < wZ; ++k) w += __popc(sZ[b * wZ + k]);
-        const int bk = kBuckets - 1 - (int)(w < kBuckets - 1 ? w : kBuckets - 1);
+        const int bk = nbk - 1 - (int)(w < (uint32_t)nbk - 1 ? w : (uint32_t)nbk - 1);
         key[b] = (uint8_t)bk;
         atomicAdd(&h[bk], 1u);
         if (zero_merge) zero_merge[b] = 0u;
     }
     __syncthreads();
-    if (t < kBuckets) counts[(long long)blockIdx.x * kBuckets + t] = h[t];
+    if (t < nbk) counts[(long long)blockIdx.x * nbk + t] = h[t];
 }
 
 // Bucket offsets: workgroup k scans column k of the [chunks][256] count matrix (one thread per
@@ -200,44 +200,47 @@ __global__ __launch_bounds__(kScatThreads) void schedule_scatter_kernel(const ui
 // [chunks][256] count matrix (at most 128 KiB, L2-resident after the histogram wrote it), forms the
 // bucket totals and its own chunk prefixes in LDS, and scatters as schedule_scatter_kernel.  One
 // dependent launch fewer for the batches where the order pass is mostly launch latency (P7 65 536:
-// three passes 46 us, of which the 16-workgroup histogram 36 us, profiles/r03/).
+// three passes 46 us, of which the 16-workgroup histogram 36 us, profiles/r03/).  It also sizes the
+// buckets to the largest possible weight (P7: mX + mZ + 1 = 43 instead of 256: the count matrix
+// each workgroup reads shrinks with them).
 constexpr int kMaxFusedChunks = QEC_SCHED_FUSED_MAX;
 __global__ __launch_bounds__(kScatThreads) void schedule_scatter_fused_kernel(const uint8_t* __restrict__ key, long long B,
-                                                                            int chunk, int nch,
+                                                                            int chunk, int nch, int nbk,
                                                                             const uint32_t* __restrict__ counts,
                                                                             int32_t* __restrict__ perm)
 {
-    constexpr int kParts = kScatThreads / kBuckets;
-    __shared__ uint32_t tot[kParts][kBuckets], pre[kParts][kBuckets];
+    __shared__ uint32_t tot[kScatThreads], pre[kScatThreads];  // [part][bucket], part * nbk + k = t
     __shared__ uint32_t start[kBuckets];
     __shared__ uint32_t cur[kBuckets];
     const int t = threadIdx.x;
     const int c = blockIdx.x;
-    const int k = t % kBuckets, part = t / kBuckets;
-    uint32_t all = 0, before = 0;
-    for (int ch = part; ch < nch; ch += kParts) {
-        const uint32_t v = counts[(long long)ch * kBuckets + k];
-        all += v;
-        before += ch < c ? v : 0u;
+    const int parts = kScatThreads / nbk;  // threads (k, part): bucket k's counts over chunks part, part + parts, ...
+    const int k = t % nbk, part = t / nbk;
+    if (part < parts) {
+        uint32_t all = 0, before = 0;
+        for (int ch = part; ch < nch; ch += parts) {
+            const uint32_t v = counts[(long long)ch * nbk + k];
+            all += v;
+            before += ch < c ? v : 0u;
+        }
+        tot[t] = all;
+        pre[t] = before;
     }
-    tot[part][k] = all;
-    pre[part][k] = before;
     __syncthreads();
     uint32_t mine = 0;
-    if (t < kBuckets) {
+    if (t < nbk) {
         uint32_t a = 0;
-#pragma unroll
-        for (int q = 0; q < kParts; ++q) { a += tot[q][t]; mine += pre[q][t]; }
+        for (int q = 0; q < parts; ++q) { a += tot[q * nbk + t]; mine += pre[q * nbk + t]; }
         start[t] = a;
     }
     __syncthreads();
-    for (int o = 1; o < kBuckets; o <<= 1) {  // inclusive scan of the bucket totals, heaviest first
-        const uint32_t add = (t < kBuckets && t >= o) ? start[t - o] : 0u;
+    for (int o = 1; o < nbk; o <<= 1) {  // inclusive scan of the bucket totals, heaviest first
+        const uint32_t add = (t < nbk && t >= o) ? start[t - o] : 0u;
         __syncthreads();
-        if (t < kBuckets) start[t] += add;
+        if (t < nbk) start[t] += add;
         __syncthreads();
     }
-    if (t < kBuckets) cur[t] = (t ? start[t - 1] : 0u) + mine;
+    if (t < nbk) cur[t] = (t ? start[t - 1] : 0u) + mine;
     __syncthreads();
     const long long r0 = (long long)c * chunk;
     const long long r1 = r0 + chunk < B ? r0 + chunk : B;
@@ -293,19 +296,23 @@ int launch_schedule(const uint8_t* sX, const uint8_t* sZ, bool sbits, long long 
     uint32_t* totals = counts + (size_t)kMaxChunks * kBuckets;
     uint8_t* key = reinterpret_cast<uint8_t*>(totals + kBuckets);
     *perm_out = perm;
+    const bool fused = nch <= kMaxFusedChunks;
+    // buckets: weights 0 .. mX + mZ (fused pass), 256 for the separate offsets / scatter passes
+    int nbk = kBuckets;
+    if (fused && mX + mZ + 1 < kBuckets) nbk = mX + mZ + 1 < 32 ? 32 : mX + mZ + 1;
     if (sbits)
         hipLaunchKernelGGL(schedule_hist_bits_kernel, dim3(nch), dim3(hthreads), 0, st,
                            reinterpret_cast<const uint32_t*>(sX), reinterpret_cast<const uint32_t*>(sZ), B, (mX + 31) / 32,
-                           (mZ + 31) / 32, chunk, key, counts, zero_merge);
+                           (mZ + 31) / 32, chunk, nbk, key, counts, zero_merge);
     else if (shortrows)
-        hipLaunchKernelGGL(schedule_hist_kernel<1>, dim3(nch), dim3(hthreads), 0, st, sX, sZ, B, mX, mZ, chunk, key,
+        hipLaunchKernelGGL(schedule_hist_kernel<1>, dim3(nch), dim3(hthreads), 0, st, sX, sZ, B, mX, mZ, chunk, nbk, key,
                            counts, zero_merge);
     else
         hipLaunchKernelGGL(schedule_hist_kernel<kHistSplitLong>, dim3(nch), dim3(hthreads), 0, st, sX, sZ, B, mX, mZ,
-                           chunk, key, counts, zero_merge);
-    if (nch <= kMaxFusedChunks) {
-        hipLaunchKernelGGL(schedule_scatter_fused_kernel, dim3(nch), dim3(kScatThreads), 0, st, key, B, chunk, nch, counts,
-                           perm);
+                           chunk, nbk, key, counts, zero_merge);
+    if (fused) {
+        hipLaunchKernelGGL(schedule_scatter_fused_kernel, dim3(nch), dim3(kScatThreads), 0, st, key, B, chunk, nch, nbk,
+                           counts, perm);
     } else {
         hipLaunchKernelGGL(schedule_offsets_kernel, dim3(kBuckets), dim3(kScanThreads), 0, st, nch, counts, totals);
         hipLaunchKernelGGL(schedule_scatter_kernel, dim3(nch), dim3(kScatThreads), 0, st, key, B, chunk, counts, totals,

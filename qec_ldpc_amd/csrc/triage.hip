@@ -28,13 +28,12 @@
 namespace qec {
 
 constexpr int kTriageWaves = 4;
-constexpr int kTriageMaxRL = 128;
 
 struct TriageArgs {
     const uint32_t* sX;  // [B][wX] bit rows (bit c = check c)
     const uint32_t* sZ;  // [B][wZ]
     long long B;
-    int wX, wZ, nb, recB;
+    int wX, wZ, nb, recB;  // recB: record row stride (>= 2 nb + 1)
     uint32_t hdpatX, cvpatX, hdpatZ, cvpatZ;  // bit idx: pattern idx decides 1 / stays outside (0.01, 0.99)
     uint8_t* rec;        // [B][recB] decision records
     int32_t* iters;      // [B][2] or null
@@ -42,9 +41,9 @@ struct TriageArgs {
     int32_t* listX;      // [B] syndromes whose X sector goes on
     int32_t* listZ;
     uint32_t* counts;    // [2] list lengths (zeroed before the launch)
-    int EX[kTriageMaxRL], EZ[kTriageMaxRL];
 };
 
+// rotations of a P-bit block by compile-time amounts (the shipped codes' generator tables)
 template <int P>
 __device__ __forceinline__ uint64_t rotl(uint64_t x, int k)
 {
@@ -66,8 +65,10 @@ __device__ __forceinline__ uint64_t pattern_eval(uint32_t pat, const uint64_t (&
     uint64_t t[1 << (R - 1)];
 #pragma unroll
     for (int m = 0; m < (1 << (R - 1)); ++m) {
-        const uint64_t c0 = 0ull - (uint64_t)((pat >> (2 * m)) & 1u), c1 = 0ull - (uint64_t)((pat >> (2 * m + 1)) & 1u);
-        t[m] = (v[0] & c1) | (~v[0] & c0);
+        // leaves 0 / all-ones from the uniform pattern bits (one 32-bit mask serves both halves)
+        const uint32_t c0 = 0u - ((pat >> (2 * m)) & 1u), c1 = 0u - ((pat >> (2 * m + 1)) & 1u);
+        const uint64_t C0 = ((uint64_t)c0 << 32) | c0, C1 = ((uint64_t)c1 << 32) | c1;
+        t[m] = (v[0] & C1) | (~v[0] & C0);
     }
 #pragma unroll
     for (int j = 1; j < R; ++j)
@@ -78,11 +79,13 @@ __device__ __forceinline__ uint64_t pattern_eval(uint32_t pat, const uint64_t (&
 
 // One sector of this lane's syndrome (its bit row): the decisions hd[l] (bit j = variable (l, j)),
 // whether iteration 0 satisfies the syndrome, and whether some message lies inside (0.01, 0.99).
-template <int R, int L, int P>
-__device__ __forceinline__ bool triage_sector(const uint32_t* __restrict__ row, const int* E, uint32_t hdpat,
-                                              uint32_t cvpat, uint64_t (&hd)[L], bool& cvbad)
+template <int R, int L, int P, class EXP, int SEC>
+__device__ __forceinline__ bool triage_sector(const uint32_t* __restrict__ row, uint32_t hdpat, uint32_t cvpat,
+                                              uint64_t (&hd)[L], bool& cvbad)
 {
     static_assert(R <= 5 && P <= 64, "patterns in 32 bits, blocks in 64");
+    constexpr EXP tab = EXP::make();
+    auto E = [&](int r, int l) constexpr { return SEC ? tab.EZ[r][l] : tab.EX[r][l]; };
     constexpr uint64_t mask = P >= 64 ? ~0ull : (1ull << P) - 1ull;
     constexpr int kW = (R * P + 31) / 32;  // words of the row
     constexpr uint32_t full = R >= 5 ? 0xFFFFFFFFu : (1u << (1 << R)) - 1u;
@@ -105,7 +108,7 @@ __device__ __forceinline__ bool triage_sector(const uint32_t* __restrict__ row, 
     for (int l = 0; l < L; ++l) {
         uint64_t v[R];  // bit j: syndrome bit of check (r, (j - E[r][l]) mod P) of variable (l, j)
 #pragma unroll
-        for (int r = 0; r < R; ++r) v[r] = rotl<P>(s[r], E[r * L + l]);
+        for (int r = 0; r < R; ++r) v[r] = rotl<P>(s[r], E(r, l));
         hd[l] = hd_const ? (hdpat ? mask : 0ull) : (pattern_eval<R>(hdpat, v) & mask);
         if (cvpat != full) bad |= pattern_eval<R>(~cvpat, v);
     }
@@ -115,7 +118,7 @@ __device__ __forceinline__ bool triage_sector(const uint32_t* __restrict__ row, 
     for (int r = 0; r < R; ++r) {  // syndrome of the decision: check (r, i) XORs variables (l, (E + i) mod P)
         uint64_t par = 0;
 #pragma unroll
-        for (int l = 0; l < L; ++l) par ^= rotr<P>(hd[l], E[r * L + l]);
+        for (int l = 0; l < L; ++l) par ^= rotr<P>(hd[l], E(r, l));
         ok &= par == s[r];
     }
     return ok;
@@ -146,7 +149,7 @@ __device__ __forceinline__ void stage_sector(uint8_t* __restrict__ row, int nb, 
     for (; out < nb; ++out) row[out] = 0;
 }
 
-template <int J, int K, int L, int P>
+template <int J, int K, int L, int P, int S, int T>
 __global__ __launch_bounds__(64 * kTriageWaves) void triage_kernel(const TriageArgs a)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t tri_smem[];
@@ -161,8 +164,9 @@ __global__ __launch_bounds__(64 * kTriageWaves) void triage_kernel(const TriageA
     const long long bl = valid ? b : b0;  // clamped row (its results are discarded)
     uint64_t hdX[L], hdZ[L];
     bool cvbX = false, cvbZ = false;
-    const bool okX = triage_sector<J, L, P>(a.sX + bl * a.wX, a.EX, a.hdpatX, a.cvpatX, hdX, cvbX);
-    const bool okZ = triage_sector<K, L, P>(a.sZ + bl * a.wZ, a.EZ, a.hdpatZ, a.cvpatZ, hdZ, cvbZ);
+    using EXP = QcExponents<J, K, L, P, S, T>;
+    const bool okX = triage_sector<J, L, P, EXP, 0>(a.sX + bl * a.wX, a.hdpatX, a.cvpatX, hdX, cvbX);
+    const bool okZ = triage_sector<K, L, P, EXP, 1>(a.sZ + bl * a.wZ, a.hdpatZ, a.cvpatZ, hdZ, cvbZ);
     const bool doneX = valid && okX, doneZ = valid && okZ;
     const uint32_t fX = cvbX ? QEC_CONVERGENCE_FAIL_X : 0u, fZ = cvbZ ? QEC_CONVERGENCE_FAIL_Z : 0u;
     // record rows: both sectors' decisions (a sector that goes on is overwritten by the list decode),
@@ -172,6 +176,7 @@ __global__ __launch_bounds__(64 * kTriageWaves) void triage_kernel(const TriageA
         stage_sector<L, P>(my, nb, hdX);
         stage_sector<L, P>(my + nb, nb, hdZ);
         my[2 * nb] = (uint8_t)(fX | fZ);
+        for (int k = 2 * nb + 1; k < recB; ++k) my[k] = 0;  // row padding (word-aligned rows)
     }
     wave_sync();
     // the wave's contiguous block of records: 16-byte stores over its aligned body, bytes at the ends
@@ -214,18 +219,24 @@ __global__ __launch_bounds__(64 * kTriageWaves) void triage_kernel(const TriageA
 
 using TriageFn = void (*)(const TriageArgs);
 
+// the shipped codes, when the file's tables are its header's generator output (as bp_decode.hip's
+// GeneratedShifts variants require)
 static TriageFn triage_fn(const Code& c)
 {
-    if (c.J == 4 && c.K == 5 && c.L == 10 && c.P == 61) return triage_kernel<4, 5, 10, 61>;
-    if (c.J == 3 && c.K == 3 && c.L == 6 && c.P == 7) return triage_kernel<3, 3, 6, 7>;
-    return nullptr;
+    TriageFn fn = nullptr;
+    if (c.J == 4 && c.K == 5 && c.L == 10 && c.P == 61 && c.sigma == 9 && c.tau == 49) fn = triage_kernel<4, 5, 10, 61, 9, 49>;
+    if (c.J == 3 && c.K == 3 && c.L == 6 && c.P == 7 && c.sigma == 2 && c.tau == 3) fn = triage_kernel<3, 3, 6, 7, 2, 3>;
+    if (!fn) return nullptr;
+    std::vector<int> EX, EZ;
+    if (!generator_exponents(c.J, c.K, c.L, c.P, c.sigma, c.tau, EX, EZ) || EX != c.EX || EZ != c.EZ) return nullptr;
+    return fn;
 }
 
 bool triage_supported(const Code& c) { return c.is_qc && triage_fn(c) != nullptr; }
 
 int launch_triage(const Code& c, const uint32_t* sX, const uint32_t* sZ, long long B, const uint32_t pats[4],
                   uint8_t* rec, int32_t* iters, uint32_t* merge, int32_t* listX, int32_t* listZ, uint32_t* counts,
-                  hipStream_t st)
+                  hipStream_t st, int rec_stride)
 {
     TriageFn fn = triage_fn(c);
     if (!fn) return fail(QEC_ERR_UNSUPPORTED, "triage: no kernel for this code");
@@ -233,11 +244,9 @@ int launch_triage(const Code& c, const uint32_t* sX, const uint32_t* sZ, long lo
     TriageArgs a{};
     a.sX = sX; a.sZ = sZ; a.B = B;
     a.wX = (c.mX + 31) / 32; a.wZ = (c.mZ + 31) / 32;
-    a.nb = (c.n + 7) / 8; a.recB = 2 * a.nb + 1;
+    a.nb = (c.n + 7) / 8; a.recB = rec_stride > 0 ? rec_stride : 2 * a.nb + 1;
     a.hdpatX = pats[0]; a.cvpatX = pats[1]; a.hdpatZ = pats[2]; a.cvpatZ = pats[3];
     a.rec = rec; a.iters = iters; a.merge = merge; a.listX = listX; a.listZ = listZ; a.counts = counts;
-    for (size_t k = 0; k < c.EX.size(); ++k) a.EX[k] = c.EX[k];
-    for (size_t k = 0; k < c.EZ.size(); ++k) a.EZ[k] = c.EZ[k];
     const long long per_block = 64LL * kTriageWaves;
     const size_t smem = (size_t)kTriageWaves * (64 * a.recB + 16);
     hipLaunchKernelGGL(fn, dim3((unsigned)((B + per_block - 1) / per_block)), dim3(64 * kTriageWaves), smem, st, a);

@@ -9,6 +9,10 @@ OBJ      := build/obj
 LIB      := qec_ldpc_amd/libqecldpc.so
 OBJS     := $(OBJ)/bp_decode.o $(OBJ)/bp_decode_p61.o $(OBJ)/bp_decode_phase.o $(OBJ)/bp_sparse.o $(OBJ)/schedule.o $(OBJ)/triage.o $(OBJ)/montecarlo.o $(OBJ)/code_model.o $(OBJ)/cpu_engine.o $(OBJ)/capi.o
 HDRS     := include/qec_ldpc.h include/HostDeviceArray.h $(CSRC)/qec_internal.h $(CSRC)/qec_device.h
+# build id: hash of every library source and this Makefile (identical for every rebuild of one tree);
+# profiles/pmc_*.json carry it and bench.py uses a profile only with the library it was taken on
+SRCS     := $(sort $(wildcard $(CSRC)/*.hip $(CSRC)/*.cpp $(CSRC)/*.h)) include/qec_ldpc.h include/HostDeviceArray.h Makefile
+BUILD_ID := $(shell cat $(SRCS) | sha256sum | cut -c1-16)
 
 all: $(LIB) oracle tools/qec_ldpc tools/getstats_check
 
@@ -44,8 +48,8 @@ $(OBJ)/code_model.o: $(CSRC)/code_model.cpp $(HDRS) | $(OBJ)
 $(OBJ)/cpu_engine.o: $(CSRC)/cpu_engine.cpp $(HDRS) | $(OBJ)
 	$(HIPCC) $(HIPFLAGS) -x c++ -c $< -o $@
 
-$(OBJ)/capi.o: $(CSRC)/capi.cpp $(HDRS) | $(OBJ)
-	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
+$(OBJ)/capi.o: $(SRCS) | $(OBJ)
+	$(HIPCC) $(HIPFLAGS) -DQEC_BUILD_ID='"$(BUILD_ID)"' -x hip -c $(CSRC)/capi.cpp -o $@
 
 $(LIB): $(OBJS)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS) -Wl,--no-undefined

@@ -92,18 +92,18 @@ def shard(total, rank, world):
     return total * rank // world, total * (rank + 1) // world
 
 
-def library_sha256():
-    import hashlib
-    with open(os.path.join(ROOT, "qec_ldpc_amd", "libqecldpc.so"), "rb") as f:
-        return hashlib.sha256(f.read()).hexdigest()
+def library_build_id():
+    import qec_ldpc_amd as q
+    return q.build_id()
 
 
 def load_pmc(code_name, iters, stop, p, batch):
     """profiles/pmc_<code>_<batch>.json or profiles/pmc_<code>.json if it was collected on this
-    workload (code, iters, stop, p, batch) with this very library (tools/gpu/pmc_summary.py stamps
-    the library's sha256): a profile of another binary or batch would mis-state the roofline."""
+    workload (code, iters, stop, p, batch) with a library built from these very sources
+    (tools/gpu/pmc_summary.py stamps qec_build_id(), a hash of the sources and flags): a profile of
+    another build or batch would mis-state the roofline."""
     why = []
-    lib = library_sha256()
+    lib = library_build_id()
     for name in ("pmc_%s_%d.json" % (code_name, batch), "pmc_%s.json" % code_name):
         path = os.path.join(ROOT, "profiles", name)
         try:
@@ -115,7 +115,7 @@ def load_pmc(code_name, iters, stop, p, batch):
             why.append("%s: other workload" % name)
         elif pm.get("batch") != batch:
             why.append("%s: batch %s" % (name, pm.get("batch")))
-        elif pm.get("library_sha256") != lib:
+        elif pm.get("build_id") != lib:
             why.append("%s: collected on another build of the library" % name)
         else:
             return pm, path

@@ -94,6 +94,9 @@ typedef struct {
 /* ---- diagnostics ---------------------------------------------------------- */
 const char* qec_last_error(void);  /* message of the last failing call on this thread */
 int qec_abi_version(void);         /* QEC_LDPC_ABI_VERSION */
+/* Build id of this library: a hash of the sources and flags it was compiled from (the same for every
+ * rebuild of the same tree); rocprofv3 profiles are stamped with it (tools/gpu/pmc_summary.py). */
+const char* qec_build_id(void);
 
 /* ---- code model ----------------------------------------------------------- */
 /* Replaces Quantum_LDPC_Code::createFromFile (QEC_LDPC/Quantum_LDPC_Code.h:26-80):

@@ -30,7 +30,7 @@ OPTION = {"hard_paths": 1, "cycle_jump": 2, "schedule": 3, "sector_split": 4, "p
 
 # every symbol include/qec_ldpc.h declares
 EXPORTS = (
-    "qec_last_error", "qec_abi_version",
+    "qec_last_error", "qec_abi_version", "qec_build_id",
     "qec_code_load", "qec_code_generate", "qec_code_free", "qec_code_params", "qec_code_exponents",
     "qec_code_pcm", "qec_code_describe", "qec_code_syndrome", "qec_code_check_logical",
     "qec_decoder_create", "qec_decoder_create_engine", "qec_decoder_create_multi", "qec_decoder_destroy",
@@ -101,6 +101,7 @@ def lib():
         sig = {
             "qec_last_error": (ctypes.c_char_p, []),
             "qec_abi_version": (i, []),
+            "qec_build_id": (ctypes.c_char_p, []),
             "qec_code_load": (vp, [ctypes.c_char_p]),
             "qec_code_generate": (vp, [i, i, i, i, i, i]),
             "qec_code_free": (i, [vp]),
@@ -146,6 +147,11 @@ def lib():
 
 def last_error():
     return lib().qec_last_error().decode()
+
+
+def build_id():
+    """Hash of the sources and flags the loaded library was built from (Makefile BUILD_ID)."""
+    return lib().qec_build_id().decode()
 
 
 def _check(rc, what):

@@ -203,6 +203,10 @@ extern "C" {
 
 const char* qec_last_error(void) { return last_error_cstr(); }
 int qec_abi_version(void) { return QEC_LDPC_ABI_VERSION; }
+#ifndef QEC_BUILD_ID
+#define QEC_BUILD_ID "unknown"
+#endif
+const char* qec_build_id(void) { return QEC_BUILD_ID; }
 
 qec_code* qec_code_load(const char* path)
 {

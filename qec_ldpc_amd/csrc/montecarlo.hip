@@ -918,8 +918,10 @@ __global__ __launch_bounds__(64 * kLaneWaves) void statistics_lane_kernel(
         }
         const unsigned long long vm = __ballot(valid), sx = __ballot(dEX), sz = __ballot(dEZ);
         const unsigned long long ok = vm & ~(sx | sz);
-        c[C_WITHX] += __popcll(__ballot(ax != 0u));
-        c[C_WITHZ] += __popcll(__ballot(az != 0u));
+        // lanes past the batch end read the clamped row B - 1: their error words are masked here
+        // (their flags are already 0)
+        c[C_WITHX] += __popcll(vm & __ballot(ax != 0u));
+        c[C_WITHZ] += __popcll(vm & __ballot(az != 0u));
         c[C_SYNX] += __popcll(sx);
         c[C_SYNZ] += __popcll(sz);
         c[C_LOGICAL] += __popcll(ok & logical);

@@ -66,3 +66,17 @@ def test_decoder_create_without_gpu_fails_loudly(code_paths):
     c = q.Quantum_LDPC_Code.createFromFile(code_paths["P61"])
     with pytest.raises(q.QecError, match="HIP"):
         q.DecoderGPU(c)
+
+
+def test_build_id_matches_sources():
+    """qec_build_id() is the Makefile's hash of the library sources: the loaded library was built
+    from this tree (a stale .so, or one built from other sources, fails here)."""
+    import glob
+    import hashlib
+    csrc = os.path.join(ROOT, "qec_ldpc_amd", "csrc")
+    srcs = sorted(glob.glob(os.path.join(csrc, "*.hip")) + glob.glob(os.path.join(csrc, "*.cpp"))
+                  + glob.glob(os.path.join(csrc, "*.h")))
+    srcs += [os.path.join(ROOT, "include", "qec_ldpc.h"), os.path.join(ROOT, "include", "HostDeviceArray.h"),
+             os.path.join(ROOT, "Makefile")]
+    h = hashlib.sha256(b"".join(open(s, "rb").read() for s in srcs)).hexdigest()[:16]
+    assert q.build_id() == h

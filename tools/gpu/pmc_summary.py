@@ -22,6 +22,7 @@ import glob
 import hashlib
 import json
 import os
+import sys
 
 KERNEL = "bp_decode_kernel"
 
@@ -88,10 +89,13 @@ def main():
     per_launch = {k: round(v) for k, v in avg.items()}
     out["per_launch"] = per_launch
     # the library the counters were collected on: bench.py uses this profile only for that binary
-    lib = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))),
-                       "qec_ldpc_amd", "libqecldpc.so")
+    root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    lib = os.path.join(root, "qec_ldpc_amd", "libqecldpc.so")
     with open(lib, "rb") as fh:
         out["library_sha256"] = hashlib.sha256(fh.read()).hexdigest()
+    sys.path.insert(0, root)
+    import qec_ldpc_amd
+    out["build_id"] = qec_ldpc_amd.build_id()
     if "FETCH_SIZE" in avg and "WRITE_SIZE" in avg:
         hbm = 2.0 * avg["FETCH_SIZE"] * 1024.0 + avg["WRITE_SIZE"] * 1024.0
         out["hbm_bytes_per_launch"] = round(hbm)

@@ -142,6 +142,10 @@ namespace qec {
 #ifndef QEC_SYN_RELAUNDER
 #define QEC_SYN_RELAUNDER 1
 #endif
+//   QEC_SCALED_DIV   var passes with at most 4 factors per fold divide guard-free on 2^32-scaled folds
+#ifndef QEC_SCALED_DIV
+#define QEC_SCALED_DIV 1
+#endif
 //   QEC_COL_GROUP    columns per division guard in soft var passes (var_pass); 0: per variant
 #ifndef QEC_COL_GROUP
 #define QEC_COL_GROUP 0
@@ -227,6 +231,7 @@ struct BpArgs {
     float errorProbability;
     int maxIter, stop;
     int hardPaths;  // QEC_HP_* bits: hard-message paths / cycle jump (QEC_OPT_HARD_PATHS, QEC_OPT_CYCLE_JUMP)
+    int scaled;     // p' in [2^-26, 1/2]: var passes with at most 4 factors per fold divide guard-free (scaled_ok)
     // lane-relabelled circulant tables (see relabel() below)
     // iteration-0 tables of both sectors computed on the host (QEC_TABLE0_HOST: the same operations,
     // so the same bits, as table0_entry on the device; each workgroup copies them to LDS)
@@ -455,6 +460,24 @@ __device__ __forceinline__ bool div_short_ok(float n, float d)
     return (d >= 0x1p-98f) & ((__float_as_uint(n) - 1u) >= (__float_as_uint(0x1p-98f) - 1u));
 }
 
+// Guard-free short division by scaling (BpArgs::scaled).  Every check->variable message is g =
+// RN(0.5 + h t), h = +-1/2, t a float in [-1, 1] (check_pass, table0_entry, or exactly 0 / 1 from the
+// hard forms): g = 0 exactly when h t = -1/2, and otherwise 0.5 + h t >= 0.5 (1 - (1 - 2^-24)) = 2^-25,
+// so every nonzero g is >= 2^-25, and every nonzero 1 - g is >= 2^-24 (g <= 1 - 2^-24 when g < 1).  A
+// numerator with F factors, p' g_a g_b ..., is then +0 or >= p' 2^-25F, a denominator +0 or >=
+// (1 - p') 2^-24F: for F <= 4 and p' >= 2^-20 both are normal (>= 2^-120, resp. 2^-97) at every step of
+// their folds, and every quotient n / d >= n / 2 is normal too.  Folding from 2^32 p' and 2^32 (1 - p')
+// instead therefore gives exactly 2^32 times every fold value (scaling by a power of two commutes with
+// rounding in the normal range; nothing reaches 2^33) and the same quotient n / d, on operands
+// 2^32 n >= 2^-88 (or +0), 2^32 d in [2^-65, 2^33]: the short form's reciprocal y1 = RN(1/d) depends only
+// on d's significand (tools/kbench/div_check.hip verified every one), its residual fma(-d, q0, n) is
+// exact (normal, >= 2^-111), so Markstein's correction again gives RN(n / d) -- without any guard.  NaN
+// operands give NaN through both forms, +0 numerators +0, 0 / 0 NaN.  F = 5 (the last iteration of a
+// five-row sector) keeps the guarded form (its numerators can reach p' 2^-125, subnormal in the
+// reference's own fold).  scaled_ok: the launch-wide condition, evaluated on the host (other p' take
+// the IEEE division in those passes).
+__host__ __device__ inline bool scaled_ok(float pp) { return pp >= 0x1p-20f && pp <= 0.5f; }
+
 //   QEC_PATH_STATS   experiment builds only: count, per sector, the var-pass columns taking each
 //                    path (same / zero / short division / full division; soft or hard inputs)
 #ifndef QEC_PATH_STATS
@@ -566,7 +589,9 @@ __device__ __forceinline__ bool short_domain(const float (&msg)[R][L], float pp,
     float b = pp;
 #pragma unroll
     for (int k = 0; k < (LAST ? R : R - 1); ++k) b = b * mf;
-    return all_live_sh<SH>((int)(__float_as_uint(b) >= __float_as_uint(0x1p-98f)) & (int)zero_ok<R, LAST>(pp), live);
+    // the uniform zero_ok is AND-ed to the ballot's scalar result, not into the per-lane predicate (that
+    // materialised the predicate as an integer and back, two VALU per ballot)
+    return all_live_sh<SH>(__float_as_uint(b) >= __float_as_uint(0x1p-98f), live) & zero_ok<R, LAST>(pp);
 }
 
 // VarNodeUpdate (DecoderCPU.h:188-229) for variables (l, i): gather the R incoming
@@ -595,6 +620,10 @@ __device__ __forceinline__ uint32_t var_pass(const BpArgs& a, float (&msg)[R][L]
     // the short division's guard assumes every message is a probability in [0, 1], which
     // holds by induction when p' is (DecoderCPU.h:135-229); other p' always take the full path
     const bool pp_ok = pp >= 0.0f && pp <= 1.0f;
+    constexpr int F = LAST ? R : R - 1;  // factors per fold
+    constexpr bool kScalable = TU::kFastDiv && F <= 4 && QEC_SCALED_DIV;
+    const bool scaled = kScalable && a.scaled;  // wave-uniform (see scaled_ok)
+    const float fold0 = scaled ? one_minus_pp * 0x1p32f : one_minus_pp, fold1 = scaled ? pp * 0x1p32f : pp;
     const int P = SH::P(a);
     const int* et = SH::template table<SEC>(a);
     uint32_t hdmask = 0;
@@ -662,13 +691,13 @@ __device__ __forceinline__ uint32_t var_pass(const BpArgs& a, float (&msg)[R][L]
 #pragma unroll
                 for (int r = 0; r < R; ++r) bv[r] = 1.0f - gv[c][r];
                 if constexpr (LAST) {
-                    float P0 = one_minus_pp, P1 = pp;
+                    float P0 = fold0, P1 = fold1;
 #pragma unroll
                     for (int k = 0; k < R; ++k) { P0 = P0 * bv[k]; P1 = P1 * gv[c][k]; }
                     num[c][0] = P1;
                     den[c][0] = P0 + P1;
                 } else {
-                    float pre0 = one_minus_pp, pre1 = pp;
+                    float pre0 = fold0, pre1 = fold1;
 #pragma unroll
                     for (int j = 0; j < R; ++j) {
                         float t0 = pre0, t1 = pre1;
@@ -696,6 +725,8 @@ __device__ __forceinline__ uint32_t var_pass(const BpArgs& a, float (&msg)[R][L]
             }
             if constexpr (ALLFAST) {
                 fast = true;
+            } else if constexpr (kScalable) {
+                fast = scaled;  // no guard (scaled folds); other p' take the IEEE division
             } else if constexpr (TU::kFastDiv) {
                 if constexpr (QEC_GUARD_ZERO != 0) {
                     // numerators outside (0, 2^-98): minima of their bit patterns minus one, +0
@@ -707,7 +738,7 @@ __device__ __forceinline__ uint32_t var_pass(const BpArgs& a, float (&msg)[R][L]
                     for (int c = 0; c < CG; ++c)
 #pragma unroll
                         for (int j = 0; j < ND; ++j) nm = min(nm, __float_as_uint(num[c][j]) - 1u);
-                    fast = all_live_sh<SH>((int)(nm >= __float_as_uint(0x1p-98f) - 1u) & (int)zero_ok<R, LAST>(pp), ln.live);
+                    fast = all_live_sh<SH>(nm >= __float_as_uint(0x1p-98f) - 1u, ln.live) & zero_ok<R, LAST>(pp);
                 } else if (!zero) {
                     // the guard of every division of the group at once, as unsigned minima of bit
                     // patterns (non-negative floats order like their bits): numerators minus 1 (+0
@@ -915,7 +946,9 @@ __device__ __forceinline__ bool iteration(const BpArgs& a, float (&msg)[R][L], u
         // never end hard; skipping only delays the exact hard forms, never changes a bit)
         // hard == false here, so the soft inputs allow column groups (var_pass)
         constexpr int CG = col_group<TU, L>();
-        const bool track = LAST || n >= QEC_TRACK_FROM;
+        // and not at all when the hard-message forms are off (QEC_OPT_HARD_PATHS = 0): the test only
+        // feeds them (var_pass returns hard = false either way)
+        const bool track = (LAST || n >= QEC_TRACK_FROM) && (a.hardPaths & QEC_HP_FORMS);
         if (QEC_GUARD_GLOBAL && TU::kFastDiv && zero_ok<R, LAST>(pp) && short_domain<R, L, LAST, SH>(msg, pp, ln.live))
             hdmask = var_pass<R, L, SEC, LAST, HD, SH, TU, CG, true>(a, msg, ln, pp, one_minus_pp, hard, vagree, track);
         else
@@ -1739,6 +1772,7 @@ int launch_decode(const void* variant, const Code& c, const uint8_t* sX, const u
     a.maxIter = maxIter < 0 ? 0 : maxIter;
     a.stop = stop;
     a.hardPaths = hardPaths & (QEC_HP_FORMS | QEC_HP_CYCLE);
+    a.scaled = scaled_ok(2.0f / 3.0f * errorProbability) ? 1 : 0;
     if (QEC_TABLE0_HOST) v->fill_tab0(2.0f / 3.0f * errorProbability, a.tab0);  // p' as the kernel forms it
     relabel(c.EX.data(), c.J, c.L, c.P, v->relabel, a.SX, a.DX, a.CX);
     relabel(c.EZ.data(), c.K, c.L, c.P, v->relabel, a.SZ, a.DZ, a.CZ);
@@ -1808,6 +1842,7 @@ int launch_decode_list(const void* variant, const Code& c, const uint8_t* sX, co
     a.maxIter = maxIter < 0 ? 0 : maxIter;
     a.stop = QEC_STOP_SYNDROME;
     a.hardPaths = hardPaths & (QEC_HP_FORMS | QEC_HP_CYCLE);
+    a.scaled = scaled_ok(2.0f / 3.0f * errorProbability) ? 1 : 0;
     if (QEC_TABLE0_HOST) v->fill_tab0(2.0f / 3.0f * errorProbability, a.tab0);
     relabel(c.EX.data(), c.J, c.L, c.P, v->relabel, a.SX, a.DX, a.CX);
     relabel(c.EZ.data(), c.K, c.L, c.P, v->relabel, a.SZ, a.DZ, a.CZ);

@@ -21,8 +21,9 @@ int launch_decode(const void* variant, const Code& c, const uint8_t* sX, const u
                   uint32_t* merge, bool merge_zeroed, hipStream_t stream, int rec_stride = 0);
 size_t schedule_workspace_bytes(long long B, int mX, int mZ);
 long long schedule_max_batch();
+long long schedule_local_max_batch();
 int launch_schedule(const uint8_t* sX, const uint8_t* sZ, bool sbits, long long B, int mX, int mZ, void* ws,
-                    uint32_t* zero_merge, int32_t** perm_out, hipStream_t st);
+                    uint32_t* zero_merge, int32_t** perm_out, hipStream_t st, bool local);
 bool decode_uses_split(const void* variant, int stop, int split, long long B);
 bool decode_has_list(const void* variant);
 bool decode_pattern_masks(const void* variant, float errorProbability, uint32_t pats[4]);
@@ -79,7 +80,7 @@ struct qec_decoder {
     std::string variant_name;
     int hard_paths = 1;             // QEC_OPT_HARD_PATHS
     int cycle_jump = 1;             // QEC_OPT_CYCLE_JUMP
-    int schedule = 1;               // QEC_OPT_SCHEDULE (0 off, 1 auto, 2 always)
+    int schedule = 1;               // QEC_OPT_SCHEDULE (0 off, 1 auto, 2 always, 3 always with the local order)
     int sector_split = 1;           // QEC_OPT_SECTOR_SPLIT (0 off, 1 auto, 2 on)
     int phase_stats = 0;            // QEC_OPT_PHASE_STATS
     int triage = 1;                 // QEC_OPT_TRIAGE
@@ -446,7 +447,7 @@ int qec_decoder_set_option(qec_decoder* d, int option, int value)
     case QEC_OPT_HARD_PATHS: d->hard_paths = value != 0; return QEC_OK;
     case QEC_OPT_CYCLE_JUMP: d->cycle_jump = value != 0; return QEC_OK;
     case QEC_OPT_SCHEDULE:
-        if (value < 0 || value > 2) return fail(QEC_ERR_ARG, "qec_decoder_set_option: QEC_OPT_SCHEDULE is 0, 1 or 2");
+        if (value < 0 || value > 3) return fail(QEC_ERR_ARG, "qec_decoder_set_option: QEC_OPT_SCHEDULE is 0 .. 3");
         d->schedule = value;
         return QEC_OK;
     case QEC_OPT_SECTOR_SPLIT:
@@ -496,6 +497,9 @@ namespace {
 // 197, 0.01 124 vs 143; 262 144 at p = 0.002: 0.450 vs 0.521 ms; profiles/r02/psweep_sched{0,1}_r02s3g.json,
 // profiles/r02/cmp_options_r02s3zb.txt).
 constexpr long long kScheduleMinBatch = 4096;
+// QEC_OPT_SCHEDULE = 1 takes the one-launch local order (schedule.hip, schedule_local_kernel) up to
+// this batch size
+constexpr long long kScheduleLocalMax = 0;
 constexpr long long kScheduleMaxSingle = 1LL << 19;
 constexpr float kScheduleSyndromeMinP = 0.004f;
 constexpr float kTriageMaxP = 0.01f;  // QEC_OPT_TRIAGE = 1 triages syndrome-stop batches up to this p
@@ -563,12 +567,14 @@ int dispatch_decode(qec_decoder* d, const uint8_t* sX, const uint8_t* sZ, long l
     const bool single = 2 * c.P > 64;  // one syndrome per wave
     const bool auto_on = B >= kScheduleMinBatch && (!single || B <= kScheduleMaxSingle) &&
                          !(stop == QEC_STOP_SYNDROME && p < kScheduleSyndromeMinP);
-    if (B > 1 && B <= schedule_max_batch() && (d->schedule == 2 || (d->schedule == 1 && auto_on))) {
+    if (B > 1 && B <= schedule_max_batch() && (d->schedule >= 2 || (d->schedule == 1 && auto_on))) {
         if ((rc = ws_reserve(d->sched, schedule_workspace_bytes(B, c.mX, c.mZ), st, "decode: dispatch order")))
             return rc;
         int32_t* pm = nullptr;
         // a sector-split launch merges its flags in zeroed words: the order pass zeroes them
-        rc = launch_schedule(sX, sZ, sbits, B, c.mX, c.mZ, d->sched.data(), split ? d->merge.data() : nullptr, &pm, st);
+        const bool local = d->schedule == 3 || (d->schedule == 1 && B <= kScheduleLocalMax);
+        rc = launch_schedule(sX, sZ, sbits, B, c.mX, c.mZ, d->sched.data(), split ? d->merge.data() : nullptr, &pm, st,
+                             local);
         if (rc) return rc;
         perm = pm;
         zeroed = split;

@@ -247,6 +247,63 @@ __global__ __launch_bounds__(kScatThreads) void schedule_scatter_fused_kernel(co
     for (long long b = r0 + t; b < r1; b += kScatThreads) perm[atomicAdd(&cur[key[b]], 1u)] = (int32_t)b;
 }
 
+// The whole order pass in one launch, for small batches (where the passes above are mostly launch
+// latency): workgroup c sorts its own chunk heaviest-first in LDS and interleaves the chunks by
+// rank, perm[rho * C + c] = the chunk's rank-rho syndrome.  A wave's G consecutive slots then hold
+// syndromes of one rank from G chunks -- the same weight quantile, as a global sort gives them -- and
+// the heaviest of every chunk come first.  Chunks have S or S - 1 syndromes (the first `rem` have S),
+// so the slots rho * C + c are exactly [0, B).  No count matrix, no second pass.
+constexpr int kLocalThreads = 512;
+constexpr int kLocalMaxChunk = 2048;
+constexpr int kLocalChunks = 128;
+long long schedule_local_max_batch() { return (long long)kLocalChunks * kLocalMaxChunk; }
+template <bool BITS>
+__global__ __launch_bounds__(kLocalThreads) void schedule_local_kernel(const uint8_t* __restrict__ sX,
+                                                                     const uint8_t* __restrict__ sZ, long long B,
+                                                                     int mX, int mZ, int S, int rem, int nbk,
+                                                                     int32_t* __restrict__ perm,
+                                                                     uint32_t* __restrict__ zero_merge)
+{
+    __shared__ uint32_t h[kBuckets];
+    __shared__ uint8_t key[kLocalMaxChunk];
+    const int t = threadIdx.x;
+    const int c = blockIdx.x, C = gridDim.x;
+    const int size = c < rem ? S : S - 1;
+    const long long r0 = (long long)c * (S - 1) + (c < rem ? c : rem);
+    for (int k = t; k < nbk; k += blockDim.x) h[k] = 0;
+    __syncthreads();
+    for (int j = t; j < size; j += blockDim.x) {
+        const long long b = r0 + j;
+        uint32_t w = 0;
+        if constexpr (BITS) {
+            const uint32_t* x = reinterpret_cast<const uint32_t*>(sX) + b * mX;  // mX, mZ: words per row here
+            const uint32_t* z = reinterpret_cast<const uint32_t*>(sZ) + b * mZ;
+            for (int k = 0; k < mX; ++k) w += __popc(x[k]);
+            for (int k = 0; k < mZ; ++k) w += __popc(z[k]);
+        } else {
+            w = range_weight(sX, b * mX, b * mX + mX) + range_weight(sZ, b * mZ, b * mZ + mZ);
+        }
+        const int bk = nbk - 1 - (int)(w < (uint32_t)nbk - 1 ? w : (uint32_t)nbk - 1);
+        key[j] = (uint8_t)bk;
+        atomicAdd(&h[bk], 1u);
+        if (zero_merge) zero_merge[b] = 0u;
+    }
+    __syncthreads();
+    if (t == 0) {  // exclusive scan of at most 256 buckets (heaviest first), one lane: a few hundred cycles
+        uint32_t a = 0;
+        for (int k = 0; k < nbk; ++k) {
+            const uint32_t v = h[k];
+            h[k] = a;
+            a += v;
+        }
+    }
+    __syncthreads();
+    for (int j = t; j < size; j += blockDim.x) {
+        const uint32_t rho = atomicAdd(&h[key[j]], 1u);
+        perm[(long long)rho * C + c] = (int32_t)(r0 + j);
+    }
+}
+
 // rows per chunk: at least min_chunk (one pass of the histogram workgroup), enough that there
 // are at most kMaxChunks chunks
 // and, below that, about QEC_SCHED_TARGET_CHUNKS chunks (power-of-two sizes up to max_chunk), so a small
@@ -277,10 +334,31 @@ size_t schedule_workspace_bytes(long long B, int, int)
 // heaviest-first order of the batch.  zero_merge (nullable): B words the hist pass zeroes on
 // the way (the sector-split decode merges its two sectors' flags there, bp_decode.hip).
 int launch_schedule(const uint8_t* sX, const uint8_t* sZ, bool sbits, long long B, int mX, int mZ, void* ws,
-                    uint32_t* zero_merge, int32_t** perm_out, hipStream_t st)
+                    uint32_t* zero_merge, int32_t** perm_out, hipStream_t st, bool local)
 {
     if (B > schedule_max_batch()) return fail(QEC_ERR_ARG, "schedule: batch too large to order");
     const bool shortrows = sbits || mX + mZ <= kShortRows;
+    if (local && shortrows && B <= schedule_local_max_batch()) {
+        // one launch: C chunks of about B / C syndromes (at most kLocalMaxChunk), sorted locally and
+        // interleaved by rank (schedule_local_kernel)
+        int C = kLocalChunks;
+        while (C > 1 && (B + C - 1) / C < 256) C /= 2;
+        const long long S = (B + C - 1) / C;
+        const int rem = (int)(B - (S - 1) * C);
+        const int nbk = mX + mZ + 1 < kBuckets ? mX + mZ + 1 : kBuckets;
+        int32_t* perm = reinterpret_cast<int32_t*>(ws);
+        *perm_out = perm;
+        const int threads = S >= kLocalThreads ? kLocalThreads : (int)((S + 63) / 64 * 64);
+        if (sbits)
+            hipLaunchKernelGGL(schedule_local_kernel<true>, dim3(C), dim3(threads), 0, st, sX, sZ, B, (mX + 31) / 32,
+                               (mZ + 31) / 32, (int)S, rem, nbk, perm, zero_merge);
+        else
+            hipLaunchKernelGGL(schedule_local_kernel<false>, dim3(C), dim3(threads), 0, st, sX, sZ, B, mX, mZ, (int)S,
+                               rem, nbk, perm, zero_merge);
+        const hipError_t err = hipGetLastError();
+        if (err != hipSuccess) return fail(QEC_ERR_HIP, std::string("schedule launch: ") + hipGetErrorString(err));
+        return QEC_OK;
+    }
     int nch = 0;
     // short rows: 4096 syndromes per chunk (four per thread): the offsets and scatter passes then
     // handle a quarter of the chunks (P7 2^20: order pass 60 -> 51 us, profiles/r02/hist_ab_r02s3zj.txt;

@@ -84,6 +84,18 @@ def test_extreme_error_probability(env, p):
             check(env, key, sX, sZ, p, N, stop)
 
 
+@pytest.mark.parametrize("p", [1.4e-6, 1.5e-6, 1e-4, 0.7499999, 0.75, 0.7500001])
+def test_scaled_division_domain_edges(env, p):
+    """The guard-free scaled short division (bp_decode.hip, scaled_ok) holds for p' in [2^-20, 1/2]:
+    p' just below and above both ends (1.4e-6 / 1.5e-6 straddle 2^-20; 0.75 gives p' = 1/2), with 50
+    iterations of dense random syndromes driving messages towards 2^-25 and numerators towards their
+    lower bound; final messages compared bit for bit."""
+    for key, B in (("P7", 400), ("P61", 40)):
+        sX, sZ = mixed_inputs(env[key][0], B, 17, 0.05)
+        for stop in ("fixed", "ref"):
+            check(env, key, sX, sZ, p, 50, stop)
+
+
 @pytest.mark.parametrize("B", [1, 2, 8, 9, 10, 17, 63, 64, 65, 1000])
 def test_ragged_batches(env, B):
     """Batch sizes that leave partial wavefront groups (P7 packs 9 syndromes per wave)."""
@@ -222,7 +234,7 @@ def test_cycle_jump_bit_identical(env, key, N):
 
 
 @pytest.mark.parametrize("key", ["P7", "P61"])
-@pytest.mark.parametrize("schedule,split", [(0, 0), (0, 2), (2, 0), (2, 2)])
+@pytest.mark.parametrize("schedule,split", [(0, 0), (0, 2), (2, 0), (2, 2), (3, 0), (3, 2)])
 @pytest.mark.parametrize("B", [1, 2, 383])
 def test_schedule_and_split_bit_identical(env, key, schedule, split, B):
     """QEC_OPT_SCHEDULE (waves take syndromes heaviest-first, schedule.hip) and
@@ -256,7 +268,7 @@ def test_split_flags_unaligned_and_dirty(env, key):
     tX, tZ = torch.from_numpy(sX).to(dev), torch.from_numpy(sZ).to(dev)
     eX = torch.empty((B, code.n), dtype=torch.uint8, device=dev)
     eZ = torch.empty((B, code.n), dtype=torch.uint8, device=dev)
-    for off, sched in ((0, 0), (1, 0), (2, 0), (3, 0), (1, 2), (2, 2)):  # schedule 2: the order pass zeroes flags
+    for off, sched in ((0, 0), (1, 0), (2, 0), (3, 0), (1, 2), (2, 2), (3, 3)):  # schedule 2: the order pass zeroes flags
         buf = torch.full((B + 8,), 0xA5, dtype=torch.uint8, device=dev)
         fl = buf[off:off + B]
         dec.set_option("sector_split", 2)
@@ -276,20 +288,21 @@ def test_split_flags_unaligned_and_dirty(env, key):
 @pytest.mark.parametrize("key", ["P7", "P61"])
 def test_schedule_many_chunks_identical(env, key):
     """A ragged batch spread over many counting-sort chunks (schedule.hip) decodes to the
-    same bits sorted and in batch order."""
+    same bits sorted, in the local (rank-interleaved chunk) order and in batch order."""
     code, dec, _ = env[key]
     B = 70001
     x, z = depolarizing_errors(code.n, 99, B, 0.03)
     sX, sZ = code.syndrome(0, x), code.syndrome(1, z)
     outs = []
-    for sched in (2, 0):
+    for sched in (2, 3, 0):
         dec.set_option("schedule", sched)
         try:
             outs.append(dec.decode_batch(sX, sZ, 0.03, 20, "ref", want_iters=True))
         finally:
             dec.set_option("schedule", 1)
-    for a, b in zip(outs[0][:4], outs[1][:4]):
-        assert np.array_equal(a, b)
+    for o in outs[1:]:
+        for a, b in zip(outs[0][:4], o[:4]):
+            assert np.array_equal(a, b)
 
 
 def test_schedule_workspace_across_calls(env):

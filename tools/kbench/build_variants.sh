@@ -3,6 +3,8 @@
 # different compile flags / macros for bp_decode.hip; the other objects are shared).
 # Used by tools/kbench/compare.py on the GPU box.
 #   tools/kbench/build_variants.sh name[:flags] ...     e.g.  cur  pipe:-DQEC_PIPELINE=1
+# SRCDIR=dir builds the variants from dir/bp_decode*.hip instead (e.g. an older revision for an A/B;
+# the directory also needs qec_device.h and qec_internal.h)
 set -e
 cd "$(dirname "$0")/../.."
 HIPCC=/opt/rocm/bin/hipcc
@@ -21,14 +23,15 @@ common qec_ldpc_amd/csrc/bp_sparse.hip &
 common qec_ldpc_amd/csrc/schedule.hip &
 common qec_ldpc_amd/csrc/triage.hip &
 wait
+SRC=${SRCDIR:-qec_ldpc_amd/csrc}
 build() {
   name=$1; shift
   out=build/variants/$name
   mkdir -p $out
-  $HIPCC $BASE -DQEC_KBENCH_MINIMAL "$@" -c qec_ldpc_amd/csrc/bp_decode.hip -o $out/bp_decode.o
-  $HIPCC $BASE -DQEC_KBENCH_MINIMAL -mllvm -amdgpu-sched-strategy=iterative-minreg "$@" \
-      -c qec_ldpc_amd/csrc/bp_decode_p61.hip -o $out/bp_decode_p61.o
-  $HIPCC $BASE -DQEC_KBENCH_MINIMAL "$@" -c qec_ldpc_amd/csrc/bp_decode_phase.hip -o $out/bp_decode_phase.o
+  $HIPCC $BASE -DQEC_KBENCH_MINIMAL -I qec_ldpc_amd/csrc "$@" -c $SRC/bp_decode.hip -o $out/bp_decode.o
+  $HIPCC $BASE -DQEC_KBENCH_MINIMAL -I qec_ldpc_amd/csrc -mllvm -amdgpu-sched-strategy=iterative-minreg "$@" \
+      -c $SRC/bp_decode_p61.hip -o $out/bp_decode_p61.o
+  $HIPCC $BASE -DQEC_KBENCH_MINIMAL -I qec_ldpc_amd/csrc "$@" -c $SRC/bp_decode_phase.hip -o $out/bp_decode_phase.o
   $HIPCC --offload-arch=gfx950 -shared -fPIC -o $out/libqecldpc.so $out/bp_decode.o $out/bp_decode_p61.o \
       $out/bp_decode_phase.o $COMMON/*.o
   echo "built $name"

@@ -146,6 +146,12 @@ namespace qec {
 #ifndef QEC_SCALED_DIV
 #define QEC_SCALED_DIV 1
 #endif
+//   QEC_SOFT_STRAIGHT  soft var passes: 1 no per-column agreement branch (P61 headline +3.6 %, P7 +1 %),
+//                      2 also one division branch per pass (two copies of each var pass in the loop: P61 2x
+//                      slower, P7 -3 %; profiles/r03/cmp_soft_straight_*.txt)
+#ifndef QEC_SOFT_STRAIGHT
+#define QEC_SOFT_STRAIGHT 1
+#endif
 //   QEC_COL_GROUP    columns per division guard in soft var passes (var_pass); 0: per variant
 #ifndef QEC_COL_GROUP
 #define QEC_COL_GROUP 0
@@ -609,12 +615,13 @@ __device__ __forceinline__ bool short_domain(const float (&msg)[R][L], float pp,
 // works column by column.
 // ALLFAST: the caller proved every division of this pass inside the short form's domain
 // (short_domain below), so no column evaluates the guard: the pass is straight-line code.
-template <int R, int L, int SEC, bool LAST, bool HD, class SH, class TU, int CG = 1, bool ALLFAST = false>
+template <int R, int L, int SEC, bool LAST, bool HD, class SH, class TU, int CG = 1, bool ALLFAST = false,
+          bool SOFT_IN = false>
 __device__ __forceinline__ uint32_t var_pass(const BpArgs& a, float (&msg)[R][L], const Lane& ln, float pp,
                                              float one_minus_pp, bool& hard, bool& vagree, bool track = true)
 {
     static_assert(L % CG == 0, "column groups must tile the L columns");
-    const bool hard_in = CG == 1 && hard;
+    const bool hard_in = !SOFT_IN && CG == 1 && hard;  // SOFT_IN: the caller knows the inputs are soft
     bool vsame = true;  // this lane's variables: all R outputs equal (float compare: NaN is unequal)
     uint32_t soft_bits = 0;  // OR of bits(q - q*q) over the outputs: 0 iff all are 0 or 1
     // the short division's guard assumes every message is a probability in [0, 1], which
@@ -949,10 +956,16 @@ __device__ __forceinline__ bool iteration(const BpArgs& a, float (&msg)[R][L], u
         // and not at all when the hard-message forms are off (QEC_OPT_HARD_PATHS = 0): the test only
         // feeds them (var_pass returns hard = false either way)
         const bool track = (LAST || n >= QEC_TRACK_FROM) && (a.hardPaths & QEC_HP_FORMS);
-        if (QEC_GUARD_GLOBAL && TU::kFastDiv && zero_ok<R, LAST>(pp) && short_domain<R, L, LAST, SH>(msg, pp, ln.live))
-            hdmask = var_pass<R, L, SEC, LAST, HD, SH, TU, CG, true>(a, msg, ln, pp, one_minus_pp, hard, vagree, track);
+        // soft inputs (SOFT_IN): no per-column agreement branch; with the scaled short division in this
+        // pass (QEC_SOFT_STRAIGHT = 2) no per-column division branch either -- one branch for the pass
+        constexpr bool kStraight = QEC_SOFT_STRAIGHT >= 1;
+        constexpr bool kScal = TU::kFastDiv && (LAST ? R : R - 1) <= 4 && QEC_SCALED_DIV;
+        if (QEC_SOFT_STRAIGHT >= 2 && kScal && a.scaled)
+            hdmask = var_pass<R, L, SEC, LAST, HD, SH, TU, CG, true, true>(a, msg, ln, pp, one_minus_pp, hard, vagree, track);
+        else if (QEC_GUARD_GLOBAL && TU::kFastDiv && zero_ok<R, LAST>(pp) && short_domain<R, L, LAST, SH>(msg, pp, ln.live))
+            hdmask = var_pass<R, L, SEC, LAST, HD, SH, TU, CG, true, kStraight>(a, msg, ln, pp, one_minus_pp, hard, vagree, track);
         else
-            hdmask = var_pass<R, L, SEC, LAST, HD, SH, TU, CG>(a, msg, ln, pp, one_minus_pp, hard, vagree, track);
+            hdmask = var_pass<R, L, SEC, LAST, HD, SH, TU, CG, false, kStraight>(a, msg, ln, pp, one_minus_pp, hard, vagree, track);
     }
     if constexpr (STOP == QEC_STOP_REF) {
         if (n % 10 == 0) return group_all_sh<SH>(lane_converged<R, L>(msg), ln, P);  // DecoderCPU.h:287-290

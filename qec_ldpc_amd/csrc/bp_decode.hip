@@ -431,6 +431,8 @@ __device__ __forceinline__ bool group_all_sh(bool pred, const Lane& ln, int P)
 }
 
 __device__ __forceinline__ bool outside(float x) { return !(x > 0.01f && x < 0.99f); }
+// AND of two wave-uniform (scalar) conditions without a short-circuit branch
+__device__ __forceinline__ bool band(bool a, bool b) { return (int)a & (int)b; }
 
 // ---- correctly rounded division, with a short path -----------------------------
 // hipcc lowers the IEEE fp32 quotient n / d to 11 instructions:
@@ -597,7 +599,7 @@ __device__ __forceinline__ bool short_domain(const float (&msg)[R][L], float pp,
     for (int k = 0; k < (LAST ? R : R - 1); ++k) b = b * mf;
     // the uniform zero_ok is AND-ed to the ballot's scalar result, not into the per-lane predicate (that
     // materialised the predicate as an integer and back, two VALU per ballot)
-    return all_live_sh<SH>(__float_as_uint(b) >= __float_as_uint(0x1p-98f), live) & zero_ok<R, LAST>(pp);
+    return band(all_live_sh<SH>(__float_as_uint(b) >= __float_as_uint(0x1p-98f), live), zero_ok<R, LAST>(pp));
 }
 
 // VarNodeUpdate (DecoderCPU.h:188-229) for variables (l, i): gather the R incoming
@@ -745,7 +747,7 @@ __device__ __forceinline__ uint32_t var_pass(const BpArgs& a, float (&msg)[R][L]
                     for (int c = 0; c < CG; ++c)
 #pragma unroll
                         for (int j = 0; j < ND; ++j) nm = min(nm, __float_as_uint(num[c][j]) - 1u);
-                    fast = all_live_sh<SH>(nm >= __float_as_uint(0x1p-98f) - 1u, ln.live) & zero_ok<R, LAST>(pp);
+                    fast = band(all_live_sh<SH>(nm >= __float_as_uint(0x1p-98f) - 1u, ln.live), zero_ok<R, LAST>(pp));
                 } else if (!zero) {
                     // the guard of every division of the group at once, as unsigned minima of bit
                     // patterns (non-negative floats order like their bits): numerators minus 1 (+0

@@ -23,7 +23,7 @@ size_t schedule_workspace_bytes(long long B, int mX, int mZ);
 long long schedule_max_batch();
 long long schedule_local_max_batch();
 int launch_schedule(const uint8_t* sX, const uint8_t* sZ, bool sbits, long long B, int mX, int mZ, void* ws,
-                    uint32_t* zero_merge, int32_t** perm_out, hipStream_t st, bool local);
+                    uint32_t* zero_merge, int32_t** perm_out, hipStream_t st, int method);
 bool decode_uses_split(const void* variant, int stop, int split, long long B);
 bool decode_has_list(const void* variant);
 bool decode_pattern_masks(const void* variant, float errorProbability, uint32_t pats[4]);
@@ -497,9 +497,6 @@ namespace {
 // 197, 0.01 124 vs 143; 262 144 at p = 0.002: 0.450 vs 0.521 ms; profiles/r02/psweep_sched{0,1}_r02s3g.json,
 // profiles/r02/cmp_options_r02s3zb.txt).
 constexpr long long kScheduleMinBatch = 4096;
-// QEC_OPT_SCHEDULE = 1 takes the one-launch local order (schedule.hip, schedule_local_kernel) up to
-// this batch size
-constexpr long long kScheduleLocalMax = 0;
 constexpr long long kScheduleMaxSingle = 1LL << 19;
 constexpr float kScheduleSyndromeMinP = 0.004f;
 constexpr float kTriageMaxP = 0.01f;  // QEC_OPT_TRIAGE = 1 triages syndrome-stop batches up to this p
@@ -572,9 +569,9 @@ int dispatch_decode(qec_decoder* d, const uint8_t* sX, const uint8_t* sZ, long l
             return rc;
         int32_t* pm = nullptr;
         // a sector-split launch merges its flags in zeroed words: the order pass zeroes them
-        const bool local = d->schedule == 3 || (d->schedule == 1 && B <= kScheduleLocalMax);
+        const int method = d->schedule == 3 ? QEC_ORDER_LOCAL : QEC_ORDER_GLOBAL;
         rc = launch_schedule(sX, sZ, sbits, B, c.mX, c.mZ, d->sched.data(), split ? d->merge.data() : nullptr, &pm, st,
-                             local);
+                             method);
         if (rc) return rc;
         perm = pm;
         zeroed = split;

@@ -84,14 +84,11 @@ __device__ __forceinline__ uint32_t range_weight(const uint8_t* s, long long lo,
 // SPLIT adjacent lanes per syndrome, each summing a 1/SPLIT share of its sX row and of its sZ
 // row; the shares are added with lane shuffles
 template <int SPLIT>
-__global__ __launch_bounds__(kHistThreads) void schedule_hist_kernel(const uint8_t* __restrict__ sX,
-                                                                   const uint8_t* __restrict__ sZ, long long B,
-                                                                   int mX, int mZ, int chunk, int nbk,
-                                                                   uint8_t* __restrict__ key,
-                                                                   uint32_t* __restrict__ counts,
-                                                                   uint32_t* __restrict__ zero_merge)
+__device__ __forceinline__ void hist_body(const uint8_t* __restrict__ sX, const uint8_t* __restrict__ sZ, long long B,
+                                          int mX, int mZ, int chunk, int nbk, uint8_t* __restrict__ key,
+                                          uint32_t* __restrict__ counts, uint32_t* __restrict__ zero_merge,
+                                          uint32_t* h)
 {
-    __shared__ uint32_t h[kBuckets];
     const int t = threadIdx.x;
     const int q = t % SPLIT;
     const long long r0 = (long long)blockIdx.x * chunk;
@@ -118,16 +115,25 @@ __global__ __launch_bounds__(kHistThreads) void schedule_hist_kernel(const uint8
     if (t < nbk) counts[(long long)blockIdx.x * nbk + t] = h[t];
 }
 
-// The same weights from bit rows (sX [B][wX], sZ [B][wZ] words; the Monte-Carlo pipeline's
-// layout): one thread per syndrome, popcounts of its words.
-__global__ __launch_bounds__(kHistThreads) void schedule_hist_bits_kernel(const uint32_t* __restrict__ sX,
-                                                                        const uint32_t* __restrict__ sZ, long long B,
-                                                                        int wX, int wZ, int chunk, int nbk,
-                                                                        uint8_t* __restrict__ key,
-                                                                        uint32_t* __restrict__ counts,
-                                                                        uint32_t* __restrict__ zero_merge)
+template <int SPLIT>
+__global__ __launch_bounds__(kHistThreads) void schedule_hist_kernel(const uint8_t* __restrict__ sX,
+                                                                   const uint8_t* __restrict__ sZ, long long B,
+                                                                   int mX, int mZ, int chunk, int nbk,
+                                                                   uint8_t* __restrict__ key,
+                                                                   uint32_t* __restrict__ counts,
+                                                                   uint32_t* __restrict__ zero_merge)
 {
     __shared__ uint32_t h[kBuckets];
+    hist_body<SPLIT>(sX, sZ, B, mX, mZ, chunk, nbk, key, counts, zero_merge, h);
+}
+
+// The same weights from bit rows (sX [B][wX], sZ [B][wZ] words; the Monte-Carlo pipeline's
+// layout): one thread per syndrome, popcounts of its words.
+__device__ __forceinline__ void hist_bits_body(const uint32_t* __restrict__ sX, const uint32_t* __restrict__ sZ,
+                                               long long B, int wX, int wZ, int chunk, int nbk,
+                                               uint8_t* __restrict__ key, uint32_t* __restrict__ counts,
+                                               uint32_t* __restrict__ zero_merge, uint32_t* h)
+{
     const int t = threadIdx.x;
     const long long r0 = (long long)blockIdx.x * chunk;
     const long long r1 = r0 + chunk < B ? r0 + chunk : B;
@@ -144,6 +150,17 @@ __global__ __launch_bounds__(kHistThreads) void schedule_hist_bits_kernel(const 
     }
     __syncthreads();
     if (t < nbk) counts[(long long)blockIdx.x * nbk + t] = h[t];
+}
+
+__global__ __launch_bounds__(kHistThreads) void schedule_hist_bits_kernel(const uint32_t* __restrict__ sX,
+                                                                        const uint32_t* __restrict__ sZ, long long B,
+                                                                        int wX, int wZ, int chunk, int nbk,
+                                                                        uint8_t* __restrict__ key,
+                                                                        uint32_t* __restrict__ counts,
+                                                                        uint32_t* __restrict__ zero_merge)
+{
+    __shared__ uint32_t h[kBuckets];
+    hist_bits_body(sX, sZ, B, wX, wZ, chunk, nbk, key, counts, zero_merge, h);
 }
 
 // Bucket offsets: workgroup k scans column k of the [chunks][256] count matrix (one thread per
@@ -204,14 +221,19 @@ __global__ __launch_bounds__(kScatThreads) void schedule_scatter_kernel(const ui
 // buckets to the largest possible weight (P7: mX + mZ + 1 = 43 instead of 256: the count matrix
 // each workgroup reads shrinks with them).
 constexpr int kMaxFusedChunks = QEC_SCHED_FUSED_MAX;
-__global__ __launch_bounds__(kScatThreads) void schedule_scatter_fused_kernel(const uint8_t* __restrict__ key, long long B,
-                                                                            int chunk, int nch, int nbk,
-                                                                            const uint32_t* __restrict__ counts,
-                                                                            int32_t* __restrict__ perm)
+struct FusedLds {
+    uint32_t tot[kScatThreads], pre[kScatThreads];  // [part][bucket], part * nbk + k = t
+    uint32_t start[kBuckets];
+    uint32_t cur[kBuckets];
+};
+__device__ __forceinline__ void scatter_fused_body(const uint8_t* __restrict__ key, long long B, int chunk, int nch,
+                                                   int nbk, const uint32_t* __restrict__ counts,
+                                                   int32_t* __restrict__ perm, FusedLds& s)
 {
-    __shared__ uint32_t tot[kScatThreads], pre[kScatThreads];  // [part][bucket], part * nbk + k = t
-    __shared__ uint32_t start[kBuckets];
-    __shared__ uint32_t cur[kBuckets];
+    uint32_t* tot = s.tot;
+    uint32_t* pre = s.pre;
+    uint32_t* start = s.start;
+    uint32_t* cur = s.cur;
     const int t = threadIdx.x;
     const int c = blockIdx.x;
     const int parts = kScatThreads / nbk;  // threads (k, part): bucket k's counts over chunks part, part + parts, ...
@@ -246,6 +268,19 @@ __global__ __launch_bounds__(kScatThreads) void schedule_scatter_fused_kernel(co
     const long long r1 = r0 + chunk < B ? r0 + chunk : B;
     for (long long b = r0 + t; b < r1; b += kScatThreads) perm[atomicAdd(&cur[key[b]], 1u)] = (int32_t)b;
 }
+
+__global__ __launch_bounds__(kScatThreads) void schedule_scatter_fused_kernel(const uint8_t* __restrict__ key, long long B,
+                                                                            int chunk, int nch, int nbk,
+                                                                            const uint32_t* __restrict__ counts,
+                                                                            int32_t* __restrict__ perm)
+{
+    __shared__ FusedLds s;
+    scatter_fused_body(key, B, chunk, nch, nbk, counts, perm, s);
+}
+
+// (A cooperative single launch -- histogram, grid barrier, scatter -- was measured 4x slower than the
+// two launches at P7 65 536: 0.288 vs 0.069 ms per decode call, hipLaunchCooperativeKernel's own cost;
+// profiles/r03/cmp_coop_order_p7_65536.txt.)
 
 // The whole order pass in one launch, for small batches (where the passes above are mostly launch
 // latency): workgroup c sorts its own chunk heaviest-first in LDS and interleaves the chunks by
@@ -334,11 +369,11 @@ size_t schedule_workspace_bytes(long long B, int, int)
 // heaviest-first order of the batch.  zero_merge (nullable): B words the hist pass zeroes on
 // the way (the sector-split decode merges its two sectors' flags there, bp_decode.hip).
 int launch_schedule(const uint8_t* sX, const uint8_t* sZ, bool sbits, long long B, int mX, int mZ, void* ws,
-                    uint32_t* zero_merge, int32_t** perm_out, hipStream_t st, bool local)
+                    uint32_t* zero_merge, int32_t** perm_out, hipStream_t st, int method)
 {
     if (B > schedule_max_batch()) return fail(QEC_ERR_ARG, "schedule: batch too large to order");
     const bool shortrows = sbits || mX + mZ <= kShortRows;
-    if (local && shortrows && B <= schedule_local_max_batch()) {
+    if (method == QEC_ORDER_LOCAL && shortrows && B <= schedule_local_max_batch()) {
         // one launch: C chunks of about B / C syndromes (at most kLocalMaxChunk), sorted locally and
         // interleaved by rank (schedule_local_kernel)
         int C = kLocalChunks;

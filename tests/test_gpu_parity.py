@@ -294,7 +294,7 @@ def test_schedule_many_chunks_identical(env, key):
     x, z = depolarizing_errors(code.n, 99, B, 0.03)
     sX, sZ = code.syndrome(0, x), code.syndrome(1, z)
     outs = []
-    for sched in (2, 3, 0):
+    for sched in (2, 3, 0):  # sorted, local order, batch order
         dec.set_option("schedule", sched)
         try:
             outs.append(dec.decode_batch(sX, sZ, 0.03, 20, "ref", want_iters=True))

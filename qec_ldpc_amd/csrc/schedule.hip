@@ -27,6 +27,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 
 #include "qec_internal.h"
 
@@ -346,6 +347,15 @@ __global__ __launch_bounds__(kLocalThreads) void schedule_local_kernel(const uin
 // 16 workgroups, 36 us)
 static int chunk_of(long long B, int min_chunk, int max_chunk, int* nchunks)
 {
+    static const int forced = [] {  // QEC_SCHED_CHUNK: rows per chunk, for experiments
+        const char* e = std::getenv("QEC_SCHED_CHUNK");
+        const int v = e ? std::atoi(e) : 0;
+        return v >= 64 && v <= kMaxChunk ? v : 0;
+    }();
+    if (forced && (B + forced - 1) / forced <= kMaxChunks) {
+        *nchunks = (int)((B + forced - 1) / forced);
+        return forced;
+    }
     long long chunk = (B + kMaxChunks - 1) / kMaxChunks;
     long long want = min_chunk;
     while (want < max_chunk && want * QEC_SCHED_TARGET_CHUNKS < B) want *= 2;

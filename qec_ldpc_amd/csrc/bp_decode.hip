@@ -146,6 +146,11 @@ namespace qec {
 #ifndef QEC_SCALED_DIV
 #define QEC_SCALED_DIV 1
 #endif
+//   QEC_ASSUME_SCALED  experiment: the scaled short division without the launch-wide test (kernels then
+//                      valid only for p' in [2^-20, 1/2])
+#ifndef QEC_ASSUME_SCALED
+#define QEC_ASSUME_SCALED 0
+#endif
 //   QEC_SOFT_STRAIGHT  soft var passes: 1 no per-column agreement branch (P61 headline +3.6 %, P7 +1 %),
 //                      2 also one division branch per pass (two copies of each var pass in the loop: P61 2x
 //                      slower, P7 -3 %; profiles/r03/cmp_soft_straight_*.txt)
@@ -631,7 +636,7 @@ __device__ __forceinline__ uint32_t var_pass(const BpArgs& a, float (&msg)[R][L]
     const bool pp_ok = pp >= 0.0f && pp <= 1.0f;
     constexpr int F = LAST ? R : R - 1;  // factors per fold
     constexpr bool kScalable = TU::kFastDiv && F <= 4 && QEC_SCALED_DIV;
-    const bool scaled = kScalable && a.scaled;  // wave-uniform (see scaled_ok)
+    const bool scaled = kScalable && (QEC_ASSUME_SCALED || a.scaled);  // wave-uniform (see scaled_ok)
     const float fold0 = scaled ? one_minus_pp * 0x1p32f : one_minus_pp, fold1 = scaled ? pp * 0x1p32f : pp;
     const int P = SH::P(a);
     const int* et = SH::template table<SEC>(a);

@@ -147,7 +147,9 @@ namespace qec {
 #define QEC_SCALED_DIV 1
 #endif
 //   QEC_ASSUME_SCALED  experiment: the scaled short division without the launch-wide test (kernels then
-//                      valid only for p' in [2^-20, 1/2])
+//                      valid only for p' in [2^-20, 1/2]); straight-line soft var passes, but the P61 fixed /
+//                      reference kernels then spill 40-44 B: headline +3.6 %, full arithmetic -4 %
+//                      (profiles/r03/cmp_assume_scaled_p61.txt) -- not taken
 #ifndef QEC_ASSUME_SCALED
 #define QEC_ASSUME_SCALED 0
 #endif

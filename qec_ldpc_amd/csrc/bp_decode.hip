@@ -153,6 +153,13 @@ namespace qec {
 #ifndef QEC_ASSUME_SCALED
 #define QEC_ASSUME_SCALED 0
 #endif
+//   QEC_COL_BARRIER  a scheduling barrier after each column group of a var pass: the machine scheduler
+//                    otherwise hoists work across columns into more live registers; P61 headline +2.8 %
+//                    (+7.2 % on another box), full arithmetic +0.9 %, P7 and the other stop rules neutral
+//                    (profiles/r03/cmp_col_barrier_*.txt)
+#ifndef QEC_COL_BARRIER
+#define QEC_COL_BARRIER 1
+#endif
 //   QEC_SOFT_STRAIGHT  soft var passes: 1 no per-column agreement branch (P61 headline +3.6 %, P7 +1 %),
 //                      2 also one division branch per pass (two copies of each var pass in the loop: P61 2x
 //                      slower, P7 -3 %; profiles/r03/cmp_soft_straight_*.txt)
@@ -847,6 +854,7 @@ __device__ __forceinline__ uint32_t var_pass(const BpArgs& a, float (&msg)[R][L]
                 msg[r][l] = rot<SH>(qv[c][r], ln, sh == 0 ? 0 : P - sh);
             }
         }
+        if constexpr (QEC_COL_BARRIER) __builtin_amdgcn_sched_barrier(0);  // see QEC_COL_BARRIER
     }
     if constexpr (TU::kSaturate) {
         const bool forms = track && (a.hardPaths & QEC_HP_FORMS) && hard_ok(pp);

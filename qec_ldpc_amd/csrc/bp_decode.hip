@@ -160,6 +160,12 @@ namespace qec {
 #ifndef QEC_COL_BARRIER
 #define QEC_COL_BARRIER 1
 #endif
+//   QEC_ROW_BARRIER  -1 per variant (Tune::kRowBarrier), 0 / 1 force: a scheduling barrier after each
+//                    check-pass row.  P61 headline +2.3 % in one A/B, -0.6 % in the next (noise), full
+//                    arithmetic -1.2 %; P7 -1..-3 % (profiles/r03/cmp_row_barrier_*.txt): off everywhere
+#ifndef QEC_ROW_BARRIER
+#define QEC_ROW_BARRIER -1
+#endif
 //   QEC_SOFT_STRAIGHT  soft var passes: 1 no per-column agreement branch (P61 headline +3.6 %, P7 +1 %),
 //                      2 also one division branch per pass (two copies of each var pass in the loop: P61 2x
 //                      slower, P7 -3 %; profiles/r03/cmp_soft_straight_*.txt)
@@ -174,8 +180,9 @@ namespace qec {
 
 // Per-variant tuning: minimum waves per SIMD for the register allocator, and the options above.
 template <int MINW_, bool RELABEL_, bool ZEROSKIP_, bool FASTDIV_, bool SATURATE_ = false, bool SPLIT_ = false,
-          bool MASKSEL_ = false, int PIPE_ = 0, int WPB_ = 4, int SYNW_ = 0, int CG_ = 1>
+          bool MASKSEL_ = false, int PIPE_ = 0, int WPB_ = 4, int SYNW_ = 0, int CG_ = 1, bool ROWB_ = false>
 struct Tune {
+    static constexpr bool kRowBarrier = QEC_PICK(QEC_ROW_BARRIER, ROWB_);
     static constexpr int kColGroup = QEC_COL_GROUP > 0 ? QEC_COL_GROUP : CG_;  // columns per division guard
     static constexpr int kMinWaves = MINW_;
     static constexpr int kMinWavesSyn = SYNW_ > 0 ? SYNW_ : MINW_;  // the syndrome-stop kernels
@@ -527,7 +534,7 @@ namespace qec {
 
 // ---- one sector (X: R = J, Z: R = K) ------------------------------------
 // EqNodeUpdate (DecoderCPU.h:150-186) for checks (r, i), r = 0..R-1: lane-local.
-template <int R, int L>
+template <int R, int L, bool RB = false>
 __device__ __forceinline__ void check_pass(float (&msg)[R][L], uint32_t sbits)
 {
 #pragma unroll
@@ -556,6 +563,7 @@ __device__ __forceinline__ void check_pass(float (&msg)[R][L], uint32_t sbits)
 #pragma unroll
             for (int l = 0; l < L; ++l) msg[r][l] = out[l];
         }
+        if constexpr (RB) __builtin_amdgcn_sched_barrier(0);  // rows one at a time (Tune::kRowBarrier)
     }
 }
 
@@ -965,7 +973,7 @@ __device__ __forceinline__ bool iteration(const BpArgs& a, float (&msg)[R][L], u
         else
             hdmask = var_pass<R, L, SEC, LAST, HD, SH, TU>(a, msg, ln, pp, one_minus_pp, hard, vagree);
     } else {
-        check_pass<R, L>(msg, sbits);
+        check_pass<R, L, TU::kRowBarrier>(msg, sbits);
         // the hard-state test is skipped in the first QEC_TRACK_FROM iterations (they essentially
         // never end hard; skipping only delays the exact hard forms, never changes a bit)
         // hard == false here, so the soft inputs allow column groups (var_pass)

@@ -21,6 +21,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 
 #include "qec_device.h"
 #include "qec_internal.h"
@@ -35,6 +36,10 @@ struct TriageArgs {
     long long B;
     int wX, wZ, nb, recB;  // recB: record row stride (>= 2 nb + 1)
     uint32_t hdpatX, cvpatX, hdpatZ, cvpatZ;  // bit idx: pattern idx decides 1 / stays outside (0.01, 0.99)
+    // the same masks by count when they depend only on the number of unsatisfied checks (symmetric):
+    // bit c = the value for patterns with c ones; sym* = 0 when a mask is not symmetric (pattern trees)
+    uint32_t hdcntX, cvcntX, hdcntZ, cvcntZ;
+    int symX, symZ;
     uint8_t* rec;        // [B][recB] decision records
     int32_t* iters;      // [B][2] or null
     uint32_t* merge;     // [B]: done bit (0x100 X, 0x200 Z) + that sector's flags
@@ -77,11 +82,46 @@ __device__ __forceinline__ uint64_t pattern_eval(uint32_t pat, const uint64_t (&
     return t[0];
 }
 
+// Bit-sliced count of ones among v[0..R) (R <= 5): b[k] = bit k of the count, per bit position (full
+// and half adders on whole words).
+template <int R>
+__device__ __forceinline__ void count_ones(const uint64_t (&v)[R], uint64_t (&b)[3])
+{
+    static_assert(R >= 1 && R <= 5, "up to five rows");
+    auto fa = [](uint64_t x, uint64_t y, uint64_t z, uint64_t& s, uint64_t& c) {
+        s = x ^ y ^ z;
+        c = (x & y) | (z & (x ^ y));
+    };
+    if constexpr (R == 1) {
+        b[0] = v[0]; b[1] = 0; b[2] = 0;
+    } else if constexpr (R == 2) {
+        b[0] = v[0] ^ v[1]; b[1] = v[0] & v[1]; b[2] = 0;
+    } else if constexpr (R == 3) {
+        fa(v[0], v[1], v[2], b[0], b[1]);
+        b[2] = 0;
+    } else if constexpr (R == 4) {
+        uint64_t s, c;
+        fa(v[0], v[1], v[2], s, c);
+        b[0] = s ^ v[3];
+        const uint64_t c2 = s & v[3];
+        b[1] = c ^ c2;
+        b[2] = c & c2;
+    } else {
+        uint64_t s, c, c2;
+        fa(v[0], v[1], v[2], s, c);
+        fa(s, v[3], v[4], b[0], c2);
+        b[1] = c ^ c2;
+        b[2] = c & c2;
+    }
+}
+
 // One sector of this lane's syndrome (its bit row): the decisions hd[l] (bit j = variable (l, j)),
 // whether iteration 0 satisfies the syndrome, and whether some message lies inside (0.01, 0.99).
-template <int R, int L, int P, class EXP, int SEC>
+// SYM: the masks are symmetric (hdcnt / cvcnt by count of ones): an adder tree and a 3-level
+// multiplexer instead of the 2^R-leaf trees (P61 Z: 16 instead of 124 bit operations per block).
+template <int R, int L, int P, class EXP, int SEC, bool SYM>
 __device__ __forceinline__ bool triage_sector(const uint32_t* __restrict__ row, uint32_t hdpat, uint32_t cvpat,
-                                              uint64_t (&hd)[L], bool& cvbad)
+                                              uint32_t hdcnt, uint32_t cvcnt, uint64_t (&hd)[L], bool& cvbad)
 {
     static_assert(R <= 5 && P <= 64, "patterns in 32 bits, blocks in 64");
     constexpr EXP tab = EXP::make();
@@ -109,8 +149,15 @@ __device__ __forceinline__ bool triage_sector(const uint32_t* __restrict__ row, 
         uint64_t v[R];  // bit j: syndrome bit of check (r, (j - E[r][l]) mod P) of variable (l, j)
 #pragma unroll
         for (int r = 0; r < R; ++r) v[r] = rotl<P>(s[r], E(r, l));
-        hd[l] = hd_const ? (hdpat ? mask : 0ull) : (pattern_eval<R>(hdpat, v) & mask);
-        if (cvpat != full) bad |= pattern_eval<R>(~cvpat, v);
+        if constexpr (SYM) {
+            uint64_t b[3];
+            count_ones<R>(v, b);
+            hd[l] = hd_const ? (hdpat ? mask : 0ull) : (pattern_eval<3>(hdcnt, b) & mask);
+            if (cvpat != full) bad |= pattern_eval<3>(~cvcnt & 0xFFu, b);
+        } else {
+            hd[l] = hd_const ? (hdpat ? mask : 0ull) : (pattern_eval<R>(hdpat, v) & mask);
+            if (cvpat != full) bad |= pattern_eval<R>(~cvpat, v);
+        }
     }
     cvbad = (bad & mask) != 0ull;
     bool ok = true;
@@ -165,8 +212,16 @@ __global__ __launch_bounds__(64 * kTriageWaves) void triage_kernel(const TriageA
     uint64_t hdX[L], hdZ[L];
     bool cvbX = false, cvbZ = false;
     using EXP = QcExponents<J, K, L, P, S, T>;
-    const bool okX = triage_sector<J, L, P, EXP, 0>(a.sX + bl * a.wX, a.hdpatX, a.cvpatX, hdX, cvbX);
-    const bool okZ = triage_sector<K, L, P, EXP, 1>(a.sZ + bl * a.wZ, a.hdpatZ, a.cvpatZ, hdZ, cvbZ);
+    // symmetric masks (the usual case) take the adder form; R <= 3 gains nothing from it
+    bool okX, okZ;
+    if (J >= 4 && a.symX)
+        okX = triage_sector<J, L, P, EXP, 0, J >= 4>(a.sX + bl * a.wX, a.hdpatX, a.cvpatX, a.hdcntX, a.cvcntX, hdX, cvbX);
+    else
+        okX = triage_sector<J, L, P, EXP, 0, false>(a.sX + bl * a.wX, a.hdpatX, a.cvpatX, 0u, 0u, hdX, cvbX);
+    if (K >= 4 && a.symZ)
+        okZ = triage_sector<K, L, P, EXP, 1, K >= 4>(a.sZ + bl * a.wZ, a.hdpatZ, a.cvpatZ, a.hdcntZ, a.cvcntZ, hdZ, cvbZ);
+    else
+        okZ = triage_sector<K, L, P, EXP, 1, false>(a.sZ + bl * a.wZ, a.hdpatZ, a.cvpatZ, 0u, 0u, hdZ, cvbZ);
     const bool doneX = valid && okX, doneZ = valid && okZ;
     const uint32_t fX = cvbX ? QEC_CONVERGENCE_FAIL_X : 0u, fZ = cvbZ ? QEC_CONVERGENCE_FAIL_Z : 0u;
     // record rows: both sectors' decisions (a sector that goes on is overwritten by the list decode),
@@ -234,6 +289,25 @@ static TriageFn triage_fn(const Code& c)
 
 bool triage_supported(const Code& c) { return c.is_qc && triage_fn(c) != nullptr; }
 
+// pat (bit idx = value for pattern idx of R bits) as a function of the pattern's count of ones: out
+// bit c = the value at count c (counts above R: 0); false if two patterns with one count differ
+static bool by_count(uint32_t pat, int R, uint32_t& out)
+{
+    out = 0;
+    uint32_t seen = 0;
+    for (int idx = 0; idx < (1 << R); ++idx) {
+        const int c = __builtin_popcount((unsigned)idx);
+        const uint32_t v = (pat >> idx) & 1u;
+        if ((seen >> c) & 1u) {
+            if (((out >> c) & 1u) != v) return false;
+        } else {
+            seen |= 1u << c;
+            out |= v << c;
+        }
+    }
+    return true;
+}
+
 int launch_triage(const Code& c, const uint32_t* sX, const uint32_t* sZ, long long B, const uint32_t pats[4],
                   uint8_t* rec, int32_t* iters, uint32_t* merge, int32_t* listX, int32_t* listZ, uint32_t* counts,
                   hipStream_t st, int rec_stride)
@@ -246,6 +320,10 @@ int launch_triage(const Code& c, const uint32_t* sX, const uint32_t* sZ, long lo
     a.wX = (c.mX + 31) / 32; a.wZ = (c.mZ + 31) / 32;
     a.nb = (c.n + 7) / 8; a.recB = rec_stride > 0 ? rec_stride : 2 * a.nb + 1;
     a.hdpatX = pats[0]; a.cvpatX = pats[1]; a.hdpatZ = pats[2]; a.cvpatZ = pats[3];
+    a.symX = by_count(pats[0], c.J, a.hdcntX) && by_count(pats[1], c.J, a.cvcntX);
+    a.symZ = by_count(pats[2], c.K, a.hdcntZ) && by_count(pats[3], c.K, a.cvcntZ);
+    const char* trees = std::getenv("QEC_TRIAGE_TREES");  // tests: force the pattern-tree form
+    if (trees && trees[0] == '1') a.symX = a.symZ = 0;
     a.rec = rec; a.iters = iters; a.merge = merge; a.listX = listX; a.listZ = listZ; a.counts = counts;
     const long long per_block = 64LL * kTriageWaves;
     const size_t smem = (size_t)kTriageWaves * (64 * a.recB + 16);

@@ -83,6 +83,21 @@ def test_triage_identical_and_oracle(env, key, p):
     assert np.array_equal(out["on"][1][:n], o[3])
 
 
+@pytest.mark.parametrize("p", [0.002, 0.01, 0.05])
+def test_triage_count_form_equals_trees(env, p, monkeypatch):
+    """Symmetric pattern masks (iteration-0 decisions that depend only on the number of unsatisfied
+    checks, the usual case) take a bit-sliced adder tree in the triage kernel; the general pattern
+    trees (QEC_TRIAGE_TREES=1) give the same records and counts."""
+    code, dec, _ = env["P61"]
+    sX, sZ = inputs(code, 5001, p, 23)
+    a = decode_all(dec, code, sX, sZ, p, 50)
+    monkeypatch.setenv("QEC_TRIAGE_TREES", "1")
+    b = decode_all(dec, code, sX, sZ, p, 50)
+    for name in ("on", "off"):
+        assert np.array_equal(a[name][0], b[name][0]) and np.array_equal(a[name][1], b[name][1]), name
+    assert np.array_equal(a["on"][0], a["off"][0])
+
+
 @pytest.mark.parametrize("key", ["P7", "P61"])
 @pytest.mark.parametrize("N,B", [(2, 777), (3, 64), (1, 100), (0, 65), (50, 1), (50, 63), (50, 129)])
 def test_triage_edges(env, key, N, B):

@@ -332,6 +332,30 @@ def test_schedule_workspace_across_calls(env):
         dec.set_option("schedule", 1)
 
 
+def test_p7_order_across_calls(env):
+    """Many ordered P7 calls in a row -- batch sizes changing, the local order (schedule 3) and batch
+    order in between, the workspace growing -- each decode to the batch-order bits."""
+    code, dec, _ = env["P7"]
+    x, z = depolarizing_errors(code.n, 77, 70000, 0.03)
+    sX, sZ = code.syndrome(0, x), code.syndrome(1, z)
+    ref = {}
+    dec.set_option("schedule", 0)
+    try:
+        for B in (5000, 9001, 4097, 70000):
+            ref[B] = dec.decode_batch(sX[:B], sZ[:B], 0.03, 20, "fixed", want_iters=True)
+    finally:
+        dec.set_option("schedule", 1)
+    try:
+        for B, sched in ((5000, 2), (9001, 2), (9001, 3), (4097, 2), (70000, 2), (5000, 0), (5000, 2), (9001, 2),
+                         (70000, 1), (4097, 1)):
+            dec.set_option("schedule", sched)
+            got = dec.decode_batch(sX[:B], sZ[:B], 0.03, 20, "fixed", want_iters=True)
+            for a, b in zip(got[:4], ref[B][:4]):
+                assert np.array_equal(a, b), "B=%d schedule=%d" % (B, sched)
+    finally:
+        dec.set_option("schedule", 1)
+
+
 @pytest.mark.parametrize("key,B", [("P7", 70001), ("P7", 1024 * 1024 + 3), ("P61", 70001), ("P61", 300001)])
 def test_schedule_covers_every_syndrome(env, key, B):
     """The order pass (schedule.hip) is a permutation of the batch: with output buffers

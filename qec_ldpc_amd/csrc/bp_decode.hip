@@ -33,6 +33,7 @@
 
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 
 #include "qec_device.h"
 #include "qec_internal.h"
@@ -1885,7 +1886,12 @@ int launch_decode_list(const void* variant, const Code& c, const uint8_t* sX, co
     relabel(c.EX.data(), c.J, c.L, c.P, v->relabel, a.SX, a.DX, a.CX);
     relabel(c.EZ.data(), c.K, c.L, c.P, v->relabel, a.SZ, a.DZ, a.CZ);
     const long long need = (2 * B + a.G - 1) / a.G;  // waves for every sector
-    const long long cap = 1024LL * v->min_waves_syn;  // one per resident slot of the chip
+    static const long long rounds = [] {  // QEC_LIST_ROUNDS: grid in resident-slot rounds (experiments)
+        const char* e = std::getenv("QEC_LIST_ROUNDS");
+        const int v = e ? std::atoi(e) : 0;
+        return (long long)(v >= 1 && v <= 64 ? v : 1);
+    }();
+    const long long cap = 1024LL * v->min_waves_syn * rounds;  // one per resident slot of the chip
     const long long waves = need < cap ? need : cap;
     const int wpb = v->waves_per_block;
     const long long blocks = (waves + wpb - 1) / wpb;

@@ -32,6 +32,7 @@ int launch_decode_list(const void* variant, const Code& c, const uint8_t* sX, co
                        uint32_t* merge, const int32_t* listX, const int32_t* listZ, const uint32_t* counts,
                        hipStream_t stream, int rec_stride = 0);
 bool triage_supported(const Code& c);
+bool triage_aligned(const void* sX, const void* sZ);
 int launch_triage(const Code& c, const uint32_t* sX, const uint32_t* sZ, long long B, const uint32_t pats[4],
                   uint8_t* rec, int32_t* iters, uint32_t* merge, int32_t* listX, int32_t* listZ, uint32_t* counts,
                   hipStream_t st, int rec_stride = 0);
@@ -541,7 +542,7 @@ int dispatch_decode(qec_decoder* d, const uint8_t* sX, const uint8_t* sZ, long l
     uint32_t pats[4];
     if (d->triage && !d->phase_stats && stop == QEC_STOP_SYNDROME && sbits && rec != nullptr && q == nullptr &&
         (d->triage == 2 || p <= kTriageMaxP) &&
-        maxIter >= 2 && B < (1LL << 31) && decode_has_list(d->variant) && triage_supported(c) &&
+        maxIter >= 2 && B < (1LL << 31) && decode_has_list(d->variant) && triage_supported(c) && triage_aligned(sX, sZ) &&
         decode_pattern_masks(d->variant, p, pats)) {
         if ((rc = ws_reserve(d->merge, (size_t)B, st, "decode")) || (rc = ws_reserve(d->tlist, 2 * (size_t)B + 2, st, "decode")))
             return rc;

@@ -120,8 +120,9 @@ __device__ __forceinline__ void count_ones(const uint64_t (&v)[R], uint64_t (&b)
 // SYM: the masks are symmetric (hdcnt / cvcnt by count of ones): an adder tree and a 3-level
 // multiplexer instead of the 2^R-leaf trees (P61 Z: 16 instead of 124 bit operations per block).
 template <int R, int L, int P, class EXP, int SEC, bool SYM>
-__device__ __forceinline__ bool triage_sector(const uint32_t* __restrict__ row, uint32_t hdpat, uint32_t cvpat,
-                                              uint32_t hdcnt, uint32_t cvcnt, uint64_t (&hd)[L], bool& cvbad)
+__device__ __forceinline__ bool triage_sector(const uint32_t* __restrict__ rows, long long b, uint32_t hdpat,
+                                              uint32_t cvpat, uint32_t hdcnt, uint32_t cvcnt, uint64_t (&hd)[L],
+                                              bool& cvbad)
 {
     static_assert(R <= 5 && P <= 64, "patterns in 32 bits, blocks in 64");
     constexpr EXP tab = EXP::make();
@@ -130,8 +131,26 @@ __device__ __forceinline__ bool triage_sector(const uint32_t* __restrict__ row, 
     constexpr int kW = (R * P + 31) / 32;  // words of the row
     constexpr uint32_t full = R >= 5 ? 0xFFFFFFFFu : (1u << (1 << R)) - 1u;
     uint32_t w[kW + 2];
+    // the row, kW words at a compile-time stride from a 16-byte aligned base (launch_triage checks):
+    // 16- or 8-byte loads where the row's alignment allows (P61: X 2 x 16 B, Z 5 x 8 B instead of 18
+    // dword loads per lane)
+    const uint32_t* __restrict__ row = rows + b * kW;
+    if constexpr (kW % 4 == 0) {
 #pragma unroll
-    for (int k = 0; k < kW; ++k) w[k] = row[k];
+        for (int k = 0; k < kW; k += 4) {
+            const uint4 v = *reinterpret_cast<const uint4*>(row + k);
+            w[k] = v.x; w[k + 1] = v.y; w[k + 2] = v.z; w[k + 3] = v.w;
+        }
+    } else if constexpr (kW % 2 == 0) {
+#pragma unroll
+        for (int k = 0; k < kW; k += 2) {
+            const uint2 v = *reinterpret_cast<const uint2*>(row + k);
+            w[k] = v.x; w[k + 1] = v.y;
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < kW; ++k) w[k] = row[k];
+    }
     w[kW] = 0u;
     w[kW + 1] = 0u;
     uint64_t s[R];  // block row r: bit i = check (r, i)
@@ -196,6 +215,36 @@ __device__ __forceinline__ void stage_sector(uint8_t* __restrict__ row, int nb, 
     for (; out < nb; ++out) row[out] = 0;
 }
 
+// The whole record (eX bits, eZ bits, flags byte, zero padding) as ndw dwords into this lane's
+// dword-aligned row of the stage: dword d takes bits [32 d, 32 d + 32) of the record's bit stream, where
+// block l of sector s starts at bit 8 nb s + P l (offsets fold at compile time; every hd block is
+// already masked to its P bits).  39 ds_write_b32 per P61 record instead of 155 byte writes.
+template <int L, int P>
+__device__ __forceinline__ void stage_record_dw(uint32_t* __restrict__ row, int ndw, const uint64_t (&hdX)[L],
+                                                const uint64_t (&hdZ)[L], uint32_t flags)
+{
+    constexpr int nb = (L * P + 7) / 8;
+    constexpr int nrec = (2 * nb + 1 + 3) / 4;  // dwords holding bits, the flags byte included
+#pragma unroll
+    for (int d = 0; d < nrec; ++d) {
+        uint32_t w = 0;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+#pragma unroll
+            for (int l = 0; l < L; ++l) {
+                const int a0 = 32 * d - (8 * nb * s + P * l);  // block bit at this dword's bit 0
+                if (a0 >= P || a0 <= -32) continue;
+                const uint64_t blk = s ? hdZ[l] : hdX[l];
+                w |= a0 >= 0 ? (uint32_t)(blk >> a0) : (uint32_t)(blk << (-a0));
+            }
+        }
+        constexpr int fb = 16 * nb;  // the flags byte's first bit
+        if (fb >= 32 * d && fb < 32 * d + 32) w |= flags << (fb - 32 * d);
+        row[d] = w;
+    }
+    for (int d = nrec; d < ndw; ++d) row[d] = 0u;  // row padding
+}
+
 template <int J, int K, int L, int P, int S, int T>
 __global__ __launch_bounds__(64 * kTriageWaves) void triage_kernel(const TriageArgs a)
 {
@@ -204,34 +253,39 @@ __global__ __launch_bounds__(64 * kTriageWaves) void triage_kernel(const TriageA
     const int recB = a.recB, nb = a.nb;
     uint8_t* __restrict__ stage = tri_smem + (size_t)wv * (64 * recB + 16);
     const long long b0 = ((long long)blockIdx.x * kTriageWaves + wv) * 64;
-    if (b0 >= a.B) return;
-    const int ns = (int)(a.B - b0 < 64 ? a.B - b0 : 64);
+    // every wave reaches the workgroup barriers below (a wave past the batch end does no work)
+    const bool wlive = b0 < a.B;
+    const int ns = !wlive ? 0 : (int)(a.B - b0 < 64 ? a.B - b0 : 64);
     const long long b = b0 + lane;
     const bool valid = lane < ns;
-    const long long bl = valid ? b : b0;  // clamped row (its results are discarded)
+    const long long bl = valid ? b : wlive ? b0 : 0;  // clamped row (its results are discarded)
     uint64_t hdX[L], hdZ[L];
     bool cvbX = false, cvbZ = false;
     using EXP = QcExponents<J, K, L, P, S, T>;
     // symmetric masks (the usual case) take the adder form; R <= 3 gains nothing from it
     bool okX, okZ;
     if (J >= 4 && a.symX)
-        okX = triage_sector<J, L, P, EXP, 0, J >= 4>(a.sX + bl * a.wX, a.hdpatX, a.cvpatX, a.hdcntX, a.cvcntX, hdX, cvbX);
+        okX = triage_sector<J, L, P, EXP, 0, J >= 4>(a.sX, bl, a.hdpatX, a.cvpatX, a.hdcntX, a.cvcntX, hdX, cvbX);
     else
-        okX = triage_sector<J, L, P, EXP, 0, false>(a.sX + bl * a.wX, a.hdpatX, a.cvpatX, 0u, 0u, hdX, cvbX);
+        okX = triage_sector<J, L, P, EXP, 0, false>(a.sX, bl, a.hdpatX, a.cvpatX, 0u, 0u, hdX, cvbX);
     if (K >= 4 && a.symZ)
-        okZ = triage_sector<K, L, P, EXP, 1, K >= 4>(a.sZ + bl * a.wZ, a.hdpatZ, a.cvpatZ, a.hdcntZ, a.cvcntZ, hdZ, cvbZ);
+        okZ = triage_sector<K, L, P, EXP, 1, K >= 4>(a.sZ, bl, a.hdpatZ, a.cvpatZ, a.hdcntZ, a.cvcntZ, hdZ, cvbZ);
     else
-        okZ = triage_sector<K, L, P, EXP, 1, false>(a.sZ + bl * a.wZ, a.hdpatZ, a.cvpatZ, 0u, 0u, hdZ, cvbZ);
+        okZ = triage_sector<K, L, P, EXP, 1, false>(a.sZ, bl, a.hdpatZ, a.cvpatZ, 0u, 0u, hdZ, cvbZ);
     const bool doneX = valid && okX, doneZ = valid && okZ;
     const uint32_t fX = cvbX ? QEC_CONVERGENCE_FAIL_X : 0u, fZ = cvbZ ? QEC_CONVERGENCE_FAIL_Z : 0u;
     // record rows: both sectors' decisions (a sector that goes on is overwritten by the list decode),
     // the flags byte final when both stopped (else written by the list decode's merge)
     uint8_t* __restrict__ my = stage + lane * recB;
     if (valid) {
-        stage_sector<L, P>(my, nb, hdX);
-        stage_sector<L, P>(my + nb, nb, hdZ);
-        my[2 * nb] = (uint8_t)(fX | fZ);
-        for (int k = 2 * nb + 1; k < recB; ++k) my[k] = 0;  // row padding (word-aligned rows)
+        if ((recB & 3) == 0) {  // word-aligned rows (the Monte-Carlo pipeline's): whole dwords
+            stage_record_dw<L, P>(reinterpret_cast<uint32_t*>(my), recB >> 2, hdX, hdZ, fX | fZ);
+        } else {
+            stage_sector<L, P>(my, nb, hdX);
+            stage_sector<L, P>(my + nb, nb, hdZ);
+            my[2 * nb] = (uint8_t)(fX | fZ);
+            for (int k = 2 * nb + 1; k < recB; ++k) my[k] = 0;
+        }
     }
     wave_sync();
     // the wave's contiguous block of records: 16-byte stores over its aligned body, bytes at the ends
@@ -258,16 +312,27 @@ __global__ __launch_bounds__(64 * kTriageWaves) void triage_kernel(const TriageA
         if (a.iters != nullptr) *reinterpret_cast<int2*>(a.iters + 2 * b) = make_int2(1, 1);  // list sectors rewrite theirs
         a.merge[b] = (doneX ? 0x100u | fX : 0u) | (doneZ ? 0x200u | fZ : 0u);
     }
-    // sectors that go on: appended to the lists (one atomic per wave and sector)
+    // sectors that go on: appended to the lists with one atomic per workgroup and sector (same-address
+    // atomics serialise at L2: one per wave put ~15 k of them on two words per 2^20 batch)
+    __shared__ uint32_t wcnt[kTriageWaves][2], wgbase[2];
     const unsigned long long lt = (1ull << lane) - 1ull;
     const unsigned long long gx = __ballot(valid && !okX), gz = __ballot(valid && !okZ);
-    uint32_t baseX = 0, baseZ = 0;
     if (lane == 0) {
-        if (gx) baseX = atomicAdd(&a.counts[0], (uint32_t)__popcll(gx));
-        if (gz) baseZ = atomicAdd(&a.counts[1], (uint32_t)__popcll(gz));
+        wcnt[wv][0] = (uint32_t)__popcll(gx);
+        wcnt[wv][1] = (uint32_t)__popcll(gz);
     }
-    baseX = __shfl(baseX, 0);
-    baseZ = __shfl(baseZ, 0);
+    __syncthreads();
+    if (threadIdx.x < 2) {
+        uint32_t tot = 0;
+        for (int w = 0; w < kTriageWaves; ++w) tot += wcnt[w][threadIdx.x];
+        wgbase[threadIdx.x] = tot ? atomicAdd(&a.counts[threadIdx.x], tot) : 0u;
+    }
+    __syncthreads();
+    uint32_t baseX = wgbase[0], baseZ = wgbase[1];
+    for (int w = 0; w < wv; ++w) {
+        baseX += wcnt[w][0];
+        baseZ += wcnt[w][1];
+    }
     if ((gx >> lane) & 1ull) a.listX[baseX + __popcll(gx & lt)] = (int32_t)b;
     if ((gz >> lane) & 1ull) a.listZ[baseZ + __popcll(gz & lt)] = (int32_t)b;
 }
@@ -288,6 +353,12 @@ static TriageFn triage_fn(const Code& c)
 }
 
 bool triage_supported(const Code& c) { return c.is_qc && triage_fn(c) != nullptr; }
+
+// the kernel loads rows with 16- / 8-byte loads (triage_sector)
+bool triage_aligned(const void* sX, const void* sZ)
+{
+    return ((reinterpret_cast<uintptr_t>(sX) | reinterpret_cast<uintptr_t>(sZ)) & 15u) == 0;
+}
 
 // pat (bit idx = value for pattern idx of R bits) as a function of the pattern's count of ones: out
 // bit c = the value at count c (counts above R: 0); false if two patterns with one count differ
@@ -314,6 +385,7 @@ int launch_triage(const Code& c, const uint32_t* sX, const uint32_t* sZ, long lo
 {
     TriageFn fn = triage_fn(c);
     if (!fn) return fail(QEC_ERR_UNSUPPORTED, "triage: no kernel for this code");
+    if (!triage_aligned(sX, sZ)) return fail(QEC_ERR_ARG, "triage: bit rows must start 16-byte aligned");
     if (B <= 0) return QEC_OK;
     TriageArgs a{};
     a.sX = sX; a.sZ = sZ; a.B = B;

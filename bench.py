@@ -97,21 +97,23 @@ def library_build_id():
     return q.build_id()
 
 
-def load_pmc(code_name, iters, stop, p, batch):
-    """profiles/pmc_<code>_<batch>.json or profiles/pmc_<code>.json if it was collected on this
-    workload (code, iters, stop, p, batch) with a library built from these very sources
-    (tools/gpu/pmc_summary.py stamps qec_build_id(), a hash of the sources and flags): a profile of
-    another build or batch would mis-state the roofline."""
+def load_pmc(code_name, iters, stop, p, batch, hard_paths=1, input_form="bits"):
+    """profiles/pmc_<code>_<batch>[_hp0].json or profiles/pmc_<code>[_hp0].json if it was collected on
+    this workload (code, iters, stop, p, batch, hard paths on / off) with a library built from these
+    very sources (tools/gpu/pmc_summary.py stamps qec_build_id(), a hash of the sources and flags): a
+    profile of another build or batch would mis-state the roofline."""
     why = []
     lib = library_build_id()
-    for name in ("pmc_%s_%d.json" % (code_name, batch), "pmc_%s.json" % code_name):
+    sfx = "" if hard_paths else "_hp0"
+    for name in ("pmc_%s_%d%s.json" % (code_name, batch, sfx), "pmc_%s%s.json" % (code_name, sfx)):
         path = os.path.join(ROOT, "profiles", name)
         try:
             with open(path) as f:
                 pm = json.load(f)
         except (OSError, ValueError):
             continue
-        if pm.get("iters") != iters or pm.get("stop") != stop or abs(float(pm.get("p", -1)) - p) > 1e-12:
+        if (pm.get("iters") != iters or pm.get("stop") != stop or abs(float(pm.get("p", -1)) - p) > 1e-12
+                or int(pm.get("hard_paths", 1)) != (1 if hard_paths else 0) or pm.get("input", "bytes") != input_form):
             why.append("%s: other workload" % name)
         elif pm.get("batch") != batch:
             why.append("%s: batch %s" % (name, pm.get("batch")))
@@ -119,7 +121,7 @@ def load_pmc(code_name, iters, stop, p, batch):
             why.append("%s: collected on another build of the library" % name)
         else:
             return pm, path
-    return None, "; ".join(why) or "no profiles/pmc_%s*.json" % code_name
+    return None, "; ".join(why) or "no profiles/pmc_%s*%s.json" % (code_name, sfx)
 
 
 def main():
@@ -136,6 +138,9 @@ def main():
     ap.add_argument("--stop", choices=["fixed", "ref", "syndrome"], default="fixed")
     ap.add_argument("--output", choices=["packed", "bytes"], default="packed",
                     help="decision records (default) or eX/eZ/flags byte arrays")
+    ap.add_argument("--input", choices=["bits", "bytes"], default="bits",
+                    help="syndromes as bit rows (default; SURVEY.md 8(d)'s bit-packed I/O, "
+                         "qec_decode_bits_packed_dev) or as 0/1 bytes (qec_decode_batch_packed_dev)")
     ap.add_argument("--min-seconds", type=float, default=1.0, help="sustained window / auto --steps target")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
     ap.add_argument("--no-cpu", action="store_true")
@@ -193,12 +198,21 @@ def main():
     dec.sample_syndrome_dev(SEED, lo, p, sX, sZ, stream=stream)
     its = torch.empty((B, 2), dtype=torch.int32, device=dev)
     packed = args.output == "packed"
+    bits = args.input == "bits"
+    if bits and not packed:
+        raise SystemExit("--input bits decodes into records (--output packed)")
+    sXb, sZb = bit_rows(sX), bit_rows(sZ)  # bit c of word c / 32 = check c (the Monte-Carlo pipeline's layout)
     if packed:
         rec = torch.empty((B, dec.record_bytes()), dtype=torch.uint8, device=dev)
         outs = (rec, its)
 
-        def step():
+        def step_bytes():
             dec.decode_batch_packed_dev(sX, sZ, p, iters, args.stop, rec, its, stream=stream)
+
+        def step_bits():
+            dec.decode_bits_packed_dev(sXb, sZb, p, iters, args.stop, rec, its, stream=stream)
+
+        step = step_bits if bits else step_bytes
     else:
         eX = torch.empty((B, code.n), dtype=torch.uint8, device=dev)
         eZ = torch.empty((B, code.n), dtype=torch.uint8, device=dev)
@@ -258,14 +272,20 @@ def main():
                 "syndromes resident in HBM",
         "config": {"workload": workload + ", " + stop_label, "code": code.describe(), "global_batch": global_batch,
                    "per_gpu_batch": B, "bp_iters": iters, "stop": args.stop, "p": p, "output": args.output,
-                   "parallelism": "dp%d" % world, "kernel": dec.describe(),
+                   "input": args.input,
+                   "parallelism": "dp%d" % world, "kernel": dec.describe(), "hard_paths": args.hard_paths,
                    **({"options": args.opt} if args.opt else {})},
         "p": p,
         "mean_iterations": {"X": round(it_mean[0], 4), "Z": round(it_mean[1], 4)},
         "decode_ms": round(kernel_ms, 4),
     }
-    pm, pm_path = load_pmc(args.code, iters, args.stop, p, B)
-    out["roofline"] = valu_roofline(pm, pm_path, B, kernel_ms, args.hard_paths)
+    pm, pm_path = load_pmc(args.code, iters, args.stop, p, B, args.hard_paths, args.input)
+    out["roofline"] = valu_roofline(pm, pm_path, B, kernel_ms)
+    if out["roofline"].get("traffic") is not None:
+        # SURVEY.md 8(d)'s bit-packed I/O per syndrome (syndrome bits in, correction bits out, flag byte)
+        io = -(-(code.numEqsX + code.numEqsZ) // 8) + -(-(2 * code.n) // 8) + 1
+        out["roofline"]["traffic_per_syndrome"] = round(out["roofline"]["traffic"] / B, 1)
+        out["roofline"]["io_bytes_per_syndrome_8d"] = io
     ab = algorithmic_bytes_per_syndrome(code, it_mean[0], it_mean[1]) * B
     gbs = ab / (kernel_ms * 1e-3) / 1e9
     out["roofline_hbm_alg"] = {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -279,12 +299,21 @@ def main():
             full = retime(dec, step, stream, B, outs, {"hard_paths": 0}, world=world)
             # whole job: every rank's shard at the slowest rank's kernel time
             out["value_full_arithmetic"] = full["syndromes_per_s"]
+            pmf, pmf_path = load_pmc(args.code, iters, args.stop, p, B, 0, args.input)
+            full["roofline"] = valu_roofline(pmf, pmf_path, B, full["kernel_ms"])
             ops = lane_ops_per_syndrome(code, 1) * (it_mean[0] + it_mean[1]) / 2.0
             tops = ops * B / (full["kernel_ms"] * 1e-3) / 1e12
             full["valu_lane_ops"] = {"achieved": round(tops, 2), "peak": VALU_PEAK_TOPS, "unit": "Tlane-op/s",
                                      "frac": round(tops / VALU_PEAK_TOPS, 4),
-                                     "basis": "analytical lane-ops of full-arithmetic BP (DESIGN.md section 5)"}
+                                     "basis": "secondary: analytical lane-ops of full-arithmetic BP (bench.py "
+                                              "lane_ops_per_syndrome, 6-instruction divisions); the counter "
+                                              "figure is full_arithmetic.roofline"}
             out["full_arithmetic"] = full
+        if packed:
+            # the other syndrome layout, same outputs (bytes: 549 B per P61 syndrome in, bits: 72 B)
+            other = step_bytes if bits else step_bits
+            out["other_input"] = dict(retime_step(other, stream, B, outs, world=world),
+                                      input="bytes" if bits else "bits")
             out["no_cycle_jump"] = retime(dec, step, stream, B, outs, {"cycle_jump": 0}, world=world)
         out["sector_iterations"] = phase_counts(dec, step, stream, its, B)
         pl = out["sector_iterations"].get("per_launch")
@@ -340,13 +369,13 @@ def timed_steps(step, steps, stream, dev, world):
     return elapsed, kernel_ms
 
 
-def valu_roofline(pm, path, B, kernel_ms, hard_paths):
+def valu_roofline(pm, path, B, kernel_ms):
     """VALU-issue roofline of the decode kernel: PMC SQ_INSTS_VALU (wave instructions) per
     syndrome x B, each taking VALU_ISSUE_CYCLES of a SIMD, over this run's launch time."""
     peak = SIMDS * CLOCK_GHZ * 1e9 / VALU_ISSUE_CYCLES / 1e12  # T wave-instructions/s
     base = {"bound": "valu", "peak": round(peak, 4), "unit": "Twave-instr/s",
             "peak_basis": "1024 SIMDs x 2.4 GHz / 2 cycles per wave64 VALU instruction"}
-    if pm is None or "valu_insts_per_syndrome" not in pm or not hard_paths:
+    if pm is None or "valu_insts_per_syndrome" not in pm:
         base.update({"achieved": None, "frac": None, "traffic": None,
                      "note": "no PMC profile for this workload and library (%s)" % path})
         return base
@@ -369,6 +398,40 @@ def valu_roofline(pm, path, B, kernel_ms, hard_paths):
     if pm.get("lds_issue_frac") is not None and pm.get("kernel_trace_avg_ns"):
         base["lds_issue_frac"] = round(pm["lds_issue_frac"] * pm["kernel_trace_avg_ns"] * 1e-6 / kernel_ms, 4)
     return base
+
+
+def bit_rows(s):
+    """[B, m] 0/1 bytes -> [B, ceil(m / 32)] int32 words, bit c of word c / 32 = check c."""
+    import torch
+    B, m = s.shape
+    w = -(-m // 32)
+    pad = torch.zeros((B, 32 * w), dtype=torch.int64, device=s.device)
+    pad[:, :m] = (s != 0).to(torch.int64)
+    v = (pad.view(B, w, 32) << torch.arange(32, device=s.device, dtype=torch.int64)).sum(2)
+    return torch.where(v >= 2 ** 31, v - 2 ** 32, v).to(torch.int32).contiguous()
+
+
+def retime_step(step, stream, B, outs, reps=3, world=1):
+    """Time another step function on the same batch; outputs checked against the timed step's."""
+    import torch
+    import torch.distributed as dist
+    ref = [t.clone() for t in outs]
+    step()
+    ms = []
+    for _ in range(reps):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        step()
+        b.record(stream)
+        torch.cuda.synchronize()
+        ms.append(a.elapsed_time(b))
+    same = all(torch.equal(r, t) for r, t in zip(ref, outs))
+    k = float(np.median(ms))
+    if world > 1:
+        t = torch.tensor([k, 0.0 if same else 1.0], dtype=torch.float64, device=outs[0].device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        k, same = float(t[0]), float(t[1]) == 0.0
+    return {"kernel_ms": round(k, 4), "syndromes_per_s": round(B * world / k * 1e3, 1), "identical": bool(same)}
 
 
 def retime(dec, step, stream, B, outs, opts, reps=3, world=1):
@@ -572,6 +635,32 @@ def published_blocks(device):
     return out
 
 
+def host_threads():
+    """OpenMP threads for the CPU baseline and where the number comes from: OMP_NUM_THREADS if set
+    (the GPU box sets it to its CPU share), else the smaller of the CPU affinity set and the cgroup
+    CPU quota; os.cpu_count() (the whole machine) is reported beside them."""
+    env = os.environ.get("OMP_NUM_THREADS")
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = os.cpu_count() or 1
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()
+            if q != "max":
+                quota = round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    if env and env.isdigit() and int(env) > 0:
+        n, src = int(env), "OMP_NUM_THREADS"
+    else:
+        n = max(1, min(aff, int(quota) if quota else aff))
+        src = "cgroup cpu.max quota" if quota and int(quota) < aff else "CPU affinity set"
+    return n, {"source": src, "OMP_NUM_THREADS": env, "affinity_cpus": aff, "cgroup_cpu_quota": quota,
+               "os_cpu_count": os.cpu_count()}
+
+
 def cpu_baseline(code, fname, sX, sZ, p, iters, args, outs, packed):
     """Oracle (CPU restatement of DecoderCPU, one decoder per OpenMP thread) on a bounded sample of
     the same batch, all host threads and 1 thread; checks the GPU's answers on that sample; and
@@ -581,7 +670,7 @@ def cpu_baseline(code, fname, sX, sZ, p, iters, args, outs, packed):
     from qec_ldpc_amd.gather import unpack_records
     import qec_ldpc_amd as q
     from qec_ldpc_amd.synthetic import depolarizing_errors
-    threads = int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)
+    threads, thread_source = host_threads()
     orc = OracleCode(code_path(fname))
     sX_h, sZ_h = sX.cpu().numpy(), sZ.cpu().numpy()
 
@@ -623,7 +712,8 @@ def cpu_baseline(code, fname, sX, sZ, p, iters, args, outs, packed):
                 break
     except OSError:
         pass
-    return {"value": round(n / dt, 2), "unit": "syndromes/s", "cores": threads, "kind": "port",
+    return {"value": round(n / dt, 2), "unit": "syndromes/s", "cores": threads, "cores_source": thread_source,
+            "kind": "port",
             "sample": "first %d syndromes of rank 0's batch, %s stop, %d iters (%.1f s)" % (n, args.stop, iters, dt),
             "cpu": cpu_model, "gpu_matches_oracle_on_sample": bool(same),
             "one_thread": {"value": round(n1 / dt1, 2), "sample": "first %d syndromes (%.1f s)" % (n1, dt1)},

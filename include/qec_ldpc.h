@@ -175,8 +175,10 @@ int qec_decoder_device(const qec_decoder* dec);         /* HIP device ordinal (o
  *   QEC_OPT_SECTOR_SPLIT (default 1): the X and Z sectors of a syndrome are decoded by two
  *     waves instead of one after the other (halves the longest wave).  The launch then zeroes
  *     flags[] first and each sector ORs in its bits.  Bit-identical either way.  0 = off,
- *     1 = the kernel variant's measured choice (on for P7, off for P61), 2 = on where the
- *     variant has split kernels (the two shipped codes).
+ *     1 = the kernel variant's measured choice, 2 = on where the variant has split kernels (the
+ *     two shipped codes), 3 = sector launches: two launches on the caller's stream, sector X then
+ *     sector Z, each kernel compiled (and its registers allocated) for its own sector only; the Z
+ *     launch ORs its flags into the byte the X launch stored (shipped codes; elsewhere as 0).
  *   QEC_OPT_PHASE_STATS (default 0; measurement only, shipped codes): launches an instrumented
  *     copy of the kernel whose iters[] output packs, per sector, the iterations executed in each
  *     phase instead of their count: soft | hard << 8 | agreed << 16 | jumped << 24 (soft: full
@@ -187,7 +189,10 @@ int qec_decoder_device(const qec_decoder* dec);         /* HIP device ordinal (o
  *     64 syndromes per wave from the syndrome patterns (triage.hip); the sectors it does not stop
  *     are compacted into lists the decode kernel then decodes (list mode).  Bit-identical either
  *     way.  0 = off (every sector in the decode kernel), 1 = when p <= 0.01 (above it most
- *     sectors go on and the ordered decode of the whole batch is faster), 2 = always. */
+ *     sectors go on and the ordered decode of the whole batch is faster), 2 = always, 3 = as 1
+ *     without the fused form.  Fused form (1, 2; depolarising qec_monte_carlo runs): sampler,
+ *     syndromes, triage and the finished samples' statistics in one kernel, so only the samples
+ *     with a sector that goes on reach HBM (list-mode decode, then their statistics). */
 enum { QEC_OPT_HARD_PATHS = 1, QEC_OPT_CYCLE_JUMP = 2, QEC_OPT_SCHEDULE = 3, QEC_OPT_SECTOR_SPLIT = 4,
        QEC_OPT_PHASE_STATS = 5, QEC_OPT_TRIAGE = 6 };
 int qec_decoder_set_option(qec_decoder* dec, int option, int value);

@@ -31,6 +31,7 @@
 // the same exact halving of the same fp32 sum.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -180,9 +181,21 @@ namespace qec {
 #define QEC_PICK(macro, dflt) ((macro) >= 0 ? (macro) != 0 : (dflt))
 
 // Per-variant tuning: minimum waves per SIMD for the register allocator, and the options above.
+//   QEC_SEQ_MINW_X / _Z  experiment: min waves per SIMD of the sector-launch kernels (MODE 3 / 4), all variants
+#ifndef QEC_SEQ_MINW_X
+#define QEC_SEQ_MINW_X 0
+#endif
+#ifndef QEC_SEQ_MINW_Z
+#define QEC_SEQ_MINW_Z 0
+#endif
 template <int MINW_, bool RELABEL_, bool ZEROSKIP_, bool FASTDIV_, bool SATURATE_ = false, bool SPLIT_ = false,
-          bool MASKSEL_ = false, int PIPE_ = 0, int WPB_ = 4, int SYNW_ = 0, int CG_ = 1, bool ROWB_ = false>
+          bool MASKSEL_ = false, int PIPE_ = 0, int WPB_ = 4, int SYNW_ = 0, int CG_ = 1, bool ROWB_ = false,
+          int MWX_ = 0, int MWZ_ = 0>
 struct Tune {
+    // sector launches (MODE 3 / 4: one kernel per sector, each compiled for its own sector only): their
+    // occupancy, 0 = kMinWaves
+    static constexpr int kMinWavesX = QEC_SEQ_MINW_X > 0 ? QEC_SEQ_MINW_X : MWX_ > 0 ? MWX_ : MINW_;
+    static constexpr int kMinWavesZ = QEC_SEQ_MINW_Z > 0 ? QEC_SEQ_MINW_Z : MWZ_ > 0 ? MWZ_ : MINW_;
     static constexpr bool kRowBarrier = QEC_PICK(QEC_ROW_BARRIER, ROWB_);
     static constexpr int kColGroup = QEC_COL_GROUP > 0 ? QEC_COL_GROUP : CG_;  // columns per division guard
     static constexpr int kMinWaves = MINW_;
@@ -195,6 +208,20 @@ struct Tune {
     static constexpr bool kZeroSkip = QEC_PICK(QEC_ZEROSKIP, ZEROSKIP_);
     static constexpr bool kFastDiv = QEC_PICK(QEC_FASTDIV, FASTDIV_);
     static constexpr bool kSaturate = QEC_PICK(QEC_SATURATE, SATURATE_);
+    static constexpr bool kAgreeSyn = false;  // the syndrome stop takes the agreement test (kAgree)
+};
+
+//   QEC_LIST_MINW_P61 / _P7   min waves per SIMD of the list-mode kernels (ListTune); QEC_LIST_AGREE 0: no
+//                             agreement test / cycle jump there
+#ifndef QEC_LIST_AGREE
+#define QEC_LIST_AGREE 0
+#endif
+// The list-mode (MODE 2) tuning of a variant: its own occupancy and the agreement test with the cycle
+// jump under the syndrome stop (see kAgree).
+template <class TU, int LW>
+struct ListTune : TU {
+    static constexpr int kMinWavesSyn = LW;
+    static constexpr bool kAgreeSyn = QEC_LIST_AGREE != 0;
 };
 
 // the largest divisor of L not above the variant's column-group size
@@ -259,7 +286,7 @@ struct BpArgs {
     float errorProbability;
     int maxIter, stop;
     int hardPaths;  // QEC_HP_* bits: hard-message paths / cycle jump (QEC_OPT_HARD_PATHS, QEC_OPT_CYCLE_JUMP)
-    int scaled;     // p' in [2^-26, 1/2]: var passes with at most 4 factors per fold divide guard-free (scaled_ok)
+    int scaled;     // p' in [2^-20, 1/2] (scaled_ok): var passes with at most 4 factors per fold divide guard-free
     // lane-relabelled circulant tables (see relabel() below)
     // iteration-0 tables of both sectors computed on the host (QEC_TABLE0_HOST: the same operations,
     // so the same bits, as table0_entry on the device; each workgroup copies them to LDS)
@@ -939,12 +966,15 @@ __device__ __forceinline__ bool lane_syndrome_ok(const BpArgs& a, uint32_t hdmas
 // Whether a hard sector first tries the whole-sector agreement test (var_pass_agree, the entry to
 // the cycle jump).  Not for the syndrome stop rule: there it costs more than it saves -- with it the
 // P61 kernel spills at 128 VGPRs, without it P61 decodes 4-15 % faster at p = 0.1 .. 0.002 and P7
-// 7 % (tools/gpu/run_syn_variants.sh, profiles/r02/syn_variants_r02s3h.txt); sectors that never
+// 7 % (profiles/r02/syn_variants_r02s3h.txt); sectors that never
 // satisfy their syndrome then run their hard iterations instead of jumping (same outputs).
-template <int STOP>
+// The list-mode kernels (ListTune: their own, lower occupancy, so no spills) take it: they decode the
+// few sectors the triage passed on, latency-bound, and the sectors that never satisfy their syndrome
+// would otherwise run all their hard iterations to the cap one by one.
+template <int STOP, class TU>
 constexpr bool kAgree()
 {
-    return QEC_AGREE && (STOP != QEC_STOP_SYNDROME || QEC_AGREE_SYN);
+    return QEC_AGREE && (STOP != QEC_STOP_SYNDROME || QEC_AGREE_SYN || TU::kAgreeSyn);
 }
 
 // One BP iteration; returns true if this group stops after it.
@@ -968,7 +998,7 @@ __device__ __forceinline__ bool iteration(const BpArgs& a, float (&msg)[R][L], u
     vagree = false;
     if (TU::kSaturate && hard) {
         check_pass_hard<R, L>(msg, sbits);  // outputs are hard too: hard stays set for the var pass
-        agreed = kAgree<STOP>() && (LAST || R >= 2) && var_pass_agree<R, L, SEC, HD, SH>(a, msg, ln, hdmask);
+        agreed = kAgree<STOP, TU>() && (LAST || R >= 2) && var_pass_agree<R, L, SEC, HD, SH>(a, msg, ln, hdmask);
         if (agreed)
             vagree = true;
         else
@@ -1436,13 +1466,19 @@ __device__ __forceinline__ void decode_sector(const BpArgs& a, Lane& ln, uint32_
 template <class TU>
 constexpr int waves_per_block() { return QEC_WAVES_PER_BLOCK > 0 ? QEC_WAVES_PER_BLOCK : TU::kWavesPerBlock; }
 
-// The syndrome pair b (or, with SPLIT, its sector doX ? X : Z) of this lane's group: decode, then
-// the flags byte and iteration counts.  SPLIT: the two sectors meet in the syndrome's merge word
-// (atomicOr of flags plus a done bit; the second to arrive stores the merged byte).
-template <int RX, int RZ, int L, int STOP, class SH, class TU, bool SPLIT>
+// The syndrome pair b (or, with one sector per wave, its sector doX ? X : Z) of this lane's group:
+// decode, then the flags byte and iteration counts.  MODE (see bp_decode_kernel) 0: both sectors,
+// plain store of the flags; 1 / 2: one sector, the two meet in the syndrome's merge word (atomicOr of
+// flags plus a done bit; the second to arrive stores the merged byte); 3: sector X of a sector launch
+// (stores its flags), 4: sector Z of a sector launch, enqueued after the X launch on the same stream
+// (ORs its flags into the byte the X launch stored).  Modes 3 and 4 compile one sector only, so each
+// kernel's registers are allocated for that sector alone.
+template <int RX, int RZ, int L, int STOP, class SH, class TU, int MODE>
 __device__ __forceinline__ void decode_group(const BpArgs& a, const float* __restrict__ tab0, uint8_t* __restrict__ stage,
                                              int i, int gb, uint32_t b, bool in_range, bool doX)
 {
+    constexpr bool SPLIT = MODE != 0;
+    constexpr bool kHasX = MODE != 4, kHasZ = MODE != 3;
     constexpr int kTabX = (1 << RX) * RX;
     // p' = (2/3) p, as the reference writes it (DecoderCPU.h:259)
     const float pp = 2.0f / 3.0f * a.errorProbability;
@@ -1453,17 +1489,23 @@ __device__ __forceinline__ void decode_group(const BpArgs& a, const float* __res
 #ifndef QEC_PREFETCH_Z
 #define QEC_PREFETCH_Z 1
 #endif
+    const bool runX = kHasX && doX, runZ = kHasZ && (!doX || !SPLIT);
     // both sectors' syndrome loads are issued up front: the Z load's latency hides behind X
-    const uint32_t sbX = doX ? load_sbits<RX, 0, SH>(a, ln, b, in_range) : 0u;
-    uint32_t sbZ = (QEC_PREFETCH_Z && (!doX || !SPLIT)) ? load_sbits<RZ, 1, SH>(a, ln, b, in_range) : 0u;
-    if (doX) decode_sector<RX, L, 0, STOP, SH, TU>(a, ln, b, in_range, pp, sbX, tab0, flags, itX, stage);
-    if (!QEC_PREFETCH_Z && (!doX || !SPLIT)) sbZ = load_sbits<RZ, 1, SH>(a, ln, b, in_range);
-    if (!doX || !SPLIT)
-        decode_sector<RZ, L, 1, STOP, SH, TU>(a, ln, b, in_range, pp, sbZ, tab0 + kTabX, flags, itZ, stage);
+    const uint32_t sbX = runX ? load_sbits<RX, 0, SH>(a, ln, b, in_range) : 0u;
+    uint32_t sbZ = (QEC_PREFETCH_Z && runZ) ? load_sbits<RZ, 1, SH>(a, ln, b, in_range) : 0u;
+    if constexpr (kHasX) {
+        if (runX) decode_sector<RX, L, 0, STOP, SH, TU>(a, ln, b, in_range, pp, sbX, tab0, flags, itX, stage);
+    }
+    if constexpr (kHasZ) {
+        if (!QEC_PREFETCH_Z && runZ) sbZ = load_sbits<RZ, 1, SH>(a, ln, b, in_range);
+        if (runZ) decode_sector<RZ, L, 1, STOP, SH, TU>(a, ln, b, in_range, pp, sbZ, tab0 + kTabX, flags, itZ, stage);
+    }
     if (in_range && lane_i<SH>(ln) == 0) {
         uint8_t* fdst = a.rec != nullptr ? a.rec + b * (long long)a.recBytes + 2 * a.nb : a.flags + b;
-        if constexpr (!SPLIT) {
+        if constexpr (MODE == 0 || MODE == 3) {
             *fdst = (uint8_t)flags;
+        } else if constexpr (MODE == 4) {
+            *fdst = (uint8_t)(*fdst | flags);  // the X launch's byte (same stream, earlier launch)
         } else {
             // the two sectors meet in the syndrome's merge word: whichever finds the other's done
             // bit already set writes the merged byte
@@ -1472,8 +1514,8 @@ __device__ __forceinline__ void decode_group(const BpArgs& a, const float* __res
             if (old & (0x300u ^ mine)) *fdst = (uint8_t)((old | flags) & 0xFFu);
         }
         if (a.iters != nullptr) {
-            if (doX) a.iters[2 * b] = itX;
-            if (!doX || !SPLIT) a.iters[2 * b + 1] = itZ;
+            if (runX) a.iters[2 * b] = itX;
+            if (runZ) a.iters[2 * b + 1] = itZ;
         }
     }
 }
@@ -1481,15 +1523,22 @@ __device__ __forceinline__ void decode_group(const BpArgs& a, const float* __res
 // MODE 0: one wave decodes both sectors of its group of G syndromes; 1 (sector split): waves 2k and
 // 2k + 1 decode sectors X and Z of group k; 2 (list, after triage.hip): the sectors that went on
 // past the triage, listX [0, counts[0]) then listZ [0, counts[1]), G per wave, each wave looping over
-// them (the grid does not depend on the lists' device-side lengths); merged as in split mode.
+// them (the grid does not depend on the lists' device-side lengths); merged as in split mode;
+// 3 / 4 (sector launches): sector X, then in a second launch on the same stream sector Z, of group k
+// in wave k (decode_group).
+template <class TU, int STOP, int MODE>
+constexpr int min_waves()
+{
+    if constexpr (QEC_MIN_WAVES_PER_EU > 0) return QEC_MIN_WAVES_PER_EU;
+    if constexpr (STOP != QEC_STOP_SYNDROME && MODE == 3) return TU::kMinWavesX;
+    if constexpr (STOP != QEC_STOP_SYNDROME && MODE == 4) return TU::kMinWavesZ;
+    return STOP == QEC_STOP_SYNDROME ? TU::kMinWavesSyn + QEC_SYN_MINW_DELTA : TU::kMinWaves;
+}
 template <int RX, int RZ, int L, int STOP, class SH, class TU, int MODE>
-__global__ __launch_bounds__(64 * waves_per_block<TU>(),
-                             (QEC_MIN_WAVES_PER_EU ? QEC_MIN_WAVES_PER_EU
-                                                   : STOP == QEC_STOP_SYNDROME ? TU::kMinWavesSyn : TU::kMinWaves) +
-                                 (STOP == QEC_STOP_SYNDROME ? QEC_SYN_MINW_DELTA : 0))
+__global__ __launch_bounds__(64 * waves_per_block<TU>(), (min_waves<TU, STOP, MODE>()))
 void bp_decode_kernel(const BpArgs a)
 {
-    constexpr bool SPLIT = MODE != 0;
+    constexpr bool SPLIT = MODE == 1 || MODE == 2;
     const int lane = threadIdx.x & 63;
     const long long wave = (long long)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     const int P = SH::P(a);
@@ -1524,7 +1573,7 @@ void bp_decode_kernel(const BpArgs a)
             const long long slot = (doX ? vw : vw - wXn) * G + g;
             const bool in_range = (g < G) && (slot < (doX ? nX : nZ));
             const uint32_t b = in_range ? (uint32_t)(doX ? a.listX : a.listZ)[slot] : 0u;
-            decode_group<RX, RZ, L, STOP, SH, TU, true>(a, tab0, stage, i, gb, b, in_range, doX);
+            decode_group<RX, RZ, L, STOP, SH, TU, 2>(a, tab0, stage, i, gb, b, in_range, doX);
         }
         return;
     }
@@ -1535,8 +1584,8 @@ void bp_decode_kernel(const BpArgs a)
     // the syndrome index in 32 bits (launch_decode caps B below 2^31): a 64-bit index live across both
     // sectors spilled at 96 VGPRs
     const uint32_t b = (in_range && a.perm != nullptr) ? (uint32_t)a.perm[slot] : (uint32_t)slot;
-    const bool doX = !SPLIT || (wave & 1) == 0;  // wave-uniform
-    decode_group<RX, RZ, L, STOP, SH, TU, SPLIT>(a, tab0, stage, i, gb, b, in_range, doX);
+    const bool doX = MODE == 3 || (MODE != 4 && (!SPLIT || (wave & 1) == 0));  // wave-uniform
+    decode_group<RX, RZ, L, STOP, SH, TU, MODE>(a, tab0, stage, i, gb, b, in_range, doX);
 }
 
 // ---- variant table ----------------------------------------------------------
@@ -1549,7 +1598,14 @@ using KernelFn = void (*)(const BpArgs);
 // P7's fixed and reference stops gain nothing, but its syndrome stop does (0.087 vs 0.100 ms)
 // (profiles/r01/session7/cmp_s7u_*.txt, cmp_s7v_*.txt).  So those kernels come from there.
 // A distinct Tune type keeps the two units' kernels apart (same code, different symbols).
-using TuneP61 = Tune<5, true, false, true, true, false, true, 2, 1, 4>;
+// Sector launches (MODE 3 / 4, QEC_OPT_SECTOR_SPLIT = 3): X alone needs R L = 40 message registers, Z 50.
+#ifndef QEC_P61_MWX
+#define QEC_P61_MWX 6
+#endif
+#ifndef QEC_P61_MWZ
+#define QEC_P61_MWZ 5
+#endif
+using TuneP61 = Tune<5, true, false, true, true, false, true, 2, 1, 4, 1, false, QEC_P61_MWX, QEC_P61_MWZ>;
 struct TuneP61MinReg : TuneP61 {};
 using ShiftsP61 = GeneratedShifts<4, 5, 10, 61, 9, 49, TuneP61::kRelabel, TuneP61::kMaskSelect>;
 // P7: three columns per division guard (col_group): 0.075 vs 0.077 ms at configs[1] (65 536 @ 20), even
@@ -1563,7 +1619,16 @@ using ShiftsP7 = GeneratedShifts<3, 3, 6, 7, 2, 3, TuneP7::kRelabel, TuneP7::kMa
 #ifndef QEC_P61_SYN_MINREG
 #define QEC_P61_SYN_MINREG 0  // the P61 syndrome-stop kernels from the minreg unit too
 #endif
+#ifndef QEC_LIST_MINW_P61
+#define QEC_LIST_MINW_P61 3
+#endif
+#ifndef QEC_LIST_MINW_P7
+#define QEC_LIST_MINW_P7 5
+#endif
+using ListTuneP61 = ListTune<TuneP61, QEC_LIST_MINW_P61>;
+using ListTuneP7 = ListTune<TuneP7MinReg, QEC_LIST_MINW_P7>;
 KernelFn p61_minreg_kernel(int stop, bool split);  // bp_decode_p61.hip
+KernelFn p61_minreg_seq_kernel(int stop, int sec); // bp_decode_p61.hip
 KernelFn p7_minreg_kernel(int stop, bool split);   // bp_decode_p61.hip
 KernelFn p7_minreg_list_kernel();                  // bp_decode_p61.hip
 
@@ -1585,6 +1650,16 @@ KernelFn p61_minreg_kernel(int stop, bool split)
 #endif
     return nullptr;
 }
+KernelFn p61_minreg_seq_kernel(int stop, int sec)
+{
+    if (stop == QEC_STOP_REF)
+        return sec ? bp_decode_kernel<4, 5, 10, QEC_STOP_REF, ShiftsP61, TuneP61MinReg, 4>
+                   : bp_decode_kernel<4, 5, 10, QEC_STOP_REF, ShiftsP61, TuneP61MinReg, 3>;
+    if (stop == QEC_STOP_FIXED)
+        return sec ? bp_decode_kernel<4, 5, 10, QEC_STOP_FIXED, ShiftsP61, TuneP61MinReg, 4>
+                   : bp_decode_kernel<4, 5, 10, QEC_STOP_FIXED, ShiftsP61, TuneP61MinReg, 3>;
+    return nullptr;
+}
 KernelFn p7_minreg_kernel(int stop, bool split)
 {
     if (stop == QEC_STOP_SYNDROME)
@@ -1592,7 +1667,7 @@ KernelFn p7_minreg_kernel(int stop, bool split)
                      : bp_decode_kernel<3, 3, 6, QEC_STOP_SYNDROME, ShiftsP7, TuneP7MinReg, 0>;
     return nullptr;
 }
-KernelFn p7_minreg_list_kernel() { return bp_decode_kernel<3, 3, 6, QEC_STOP_SYNDROME, ShiftsP7, TuneP7MinReg, 2>; }
+KernelFn p7_minreg_list_kernel() { return bp_decode_kernel<3, 3, 6, QEC_STOP_SYNDROME, ShiftsP7, ListTuneP7, 2>; }
 #elif defined(QEC_PHASE_TU)
 // The instrumented kernels of the shipped codes (QEC_OPT_PHASE_STATS, one wave per syndrome):
 // iters[] reports per sector soft | hard << 8 | agreed << 16 | jumped << 24 iterations.
@@ -1624,6 +1699,8 @@ struct Variant {
     const char* name;
     KernelFn list = nullptr;  // syndrome stop, list mode (MODE 2: the sectors the triage passed on)
     int min_waves_syn = 1;    // its occupancy (waves per SIMD), for the list launch's grid
+    KernelFn seq[3][2] = {};  // sector launches (MODE 3 / 4): [stop][sector]
+    bool seq_auto = false;    // QEC_OPT_SECTOR_SPLIT = 1 takes the sector launches
 };
 
 // Both sectors' iteration-0 tables on the host, entry for entry what the device's table0_entry
@@ -1639,7 +1716,7 @@ static int fill_tab0(float pp, float* out)
     return tx + tz;
 }
 
-template <int J, int K, int L, class SH, class TU, bool WITH_SPLIT>
+template <int J, int K, int L, class SH, class TU, bool WITH_SPLIT, class TUL = TU>
 static Variant make_variant(int P, int S, int T, const char* name)
 {
     Variant v{J, K, L, P, S, T, TU::kRelabel, TU::kSplit && WITH_SPLIT, waves_per_block<TU>(),
@@ -1654,9 +1731,15 @@ static Variant make_variant(int P, int S, int T, const char* name)
         v.split[QEC_STOP_REF] = bp_decode_kernel<J, K, L, QEC_STOP_REF, SH, TU, 1>;
         v.split[QEC_STOP_FIXED] = bp_decode_kernel<J, K, L, QEC_STOP_FIXED, SH, TU, 1>;
         v.split[QEC_STOP_SYNDROME] = bp_decode_kernel<J, K, L, QEC_STOP_SYNDROME, SH, TU, 1>;
-        v.list = bp_decode_kernel<J, K, L, QEC_STOP_SYNDROME, SH, TU, 2>;
+        v.list = bp_decode_kernel<J, K, L, QEC_STOP_SYNDROME, SH, TUL, 2>;
+        v.seq[QEC_STOP_REF][0] = bp_decode_kernel<J, K, L, QEC_STOP_REF, SH, TU, 3>;
+        v.seq[QEC_STOP_REF][1] = bp_decode_kernel<J, K, L, QEC_STOP_REF, SH, TU, 4>;
+        v.seq[QEC_STOP_FIXED][0] = bp_decode_kernel<J, K, L, QEC_STOP_FIXED, SH, TU, 3>;
+        v.seq[QEC_STOP_FIXED][1] = bp_decode_kernel<J, K, L, QEC_STOP_FIXED, SH, TU, 4>;
+        v.seq[QEC_STOP_SYNDROME][0] = bp_decode_kernel<J, K, L, QEC_STOP_SYNDROME, SH, TU, 3>;
+        v.seq[QEC_STOP_SYNDROME][1] = bp_decode_kernel<J, K, L, QEC_STOP_SYNDROME, SH, TU, 4>;
     }
-    v.min_waves_syn = TU::kMinWavesSyn;
+    v.min_waves_syn = TUL::kMinWavesSyn;  // the list launch's grid (launch_decode_list)
     return v;
 }
 // Tune<min waves per SIMD, relabel, zero-skip, short division, hard-message paths, sector split,
@@ -1666,10 +1749,10 @@ static Variant rt()
 {
     return make_variant<J, K, L, RuntimeShifts, TU, false>(0, 0, 0, "wave-circulant runtime-shift");
 }
-template <int J, int K, int L, int P, int S, int T, class TU>
+template <int J, int K, int L, int P, int S, int T, class TU, class TUL = TU>
 static Variant gen()
 {
-    return make_variant<J, K, L, GeneratedShifts<J, K, L, P, S, T, TU::kRelabel, TU::kMaskSelect>, TU, true>(
+    return make_variant<J, K, L, GeneratedShifts<J, K, L, P, S, T, TU::kRelabel, TU::kMaskSelect>, TU, true, TUL>(
         P, S, T, "wave-circulant generated-shift");
 }
 
@@ -1693,13 +1776,15 @@ static Variant gen()
 // vs 131.9M syn/s with two, P7 +3 % vs four; profiles/r02/cmp_wpb_r02s3x.txt).
 static Variant gen_p61()
 {
-    Variant v = gen<4, 5, 10, 61, 9, 49, TuneP61>();
+    Variant v = gen<4, 5, 10, 61, 9, 49, TuneP61, ListTuneP61>();
     for (int stop : {QEC_STOP_REF, QEC_STOP_FIXED, QEC_STOP_SYNDROME}) v.phase[stop] = phase_kernel(61, stop);
     if (QEC_P61_MINREG) {
         for (int stop : {QEC_STOP_REF, QEC_STOP_FIXED, QEC_STOP_SYNDROME}) {
             if (stop == QEC_STOP_SYNDROME && !QEC_P61_SYN_MINREG) continue;
             v.fn[stop] = p61_minreg_kernel(stop, false);
             v.split[stop] = p61_minreg_kernel(stop, true);
+            if (stop != QEC_STOP_SYNDROME)
+                for (int sec = 0; sec < 2; ++sec) v.seq[stop][sec] = p61_minreg_seq_kernel(stop, sec);
         }
     }
     return v;
@@ -1707,12 +1792,13 @@ static Variant gen_p61()
 
 static Variant gen_p7()
 {
-    Variant v = gen<3, 3, 6, 7, 2, 3, TuneP7>();
+    Variant v = gen<3, 3, 6, 7, 2, 3, TuneP7, ListTuneP7>();
     for (int stop : {QEC_STOP_REF, QEC_STOP_FIXED, QEC_STOP_SYNDROME}) v.phase[stop] = phase_kernel(7, stop);
     if (QEC_P61_MINREG) {
         v.fn[QEC_STOP_SYNDROME] = p7_minreg_kernel(QEC_STOP_SYNDROME, false);
         v.split[QEC_STOP_SYNDROME] = p7_minreg_kernel(QEC_STOP_SYNDROME, true);
         v.list = p7_minreg_list_kernel();
+        v.min_waves_syn = ListTuneP7::kMinWavesSyn;
     }
     return v;
 }
@@ -1766,9 +1852,17 @@ const void* select_variant(const Code& c, std::string& name)
 // 2^20 1790 vs 1835 M/s split vs one wave per group; profiles/r02/p7_split_r02s3zz.txt).
 constexpr long long kSplitAutoMaxBatch = 1LL << 19;
 
+// Sector launches (QEC_OPT_SECTOR_SPLIT = 3, or 1 where the variant's measured choice, seq_auto):
+// two launches, sector X then sector Z, each kernel compiled for its own sector (no merge words).
+static bool decode_uses_seq(const Variant* v, int stop, int split)
+{
+    return (split == 3 || (split == 1 && v->seq_auto)) && v->seq[stop][0] != nullptr && v->seq[stop][1] != nullptr;
+}
+
 bool decode_uses_split(const void* variant, int stop, int split, long long B)
 {
     const Variant* v = static_cast<const Variant*>(variant);
+    if (decode_uses_seq(v, stop, split)) return false;
     return (split == 2 || (split == 1 && v->split_auto && B < kSplitAutoMaxBatch)) && v->split[stop] != nullptr;
 }
 
@@ -1795,6 +1889,7 @@ int launch_decode(const void* variant, const Code& c, const uint8_t* sX, const u
     const bool phase = (hardPaths & QEC_HP_PHASE) != 0;
     if (phase && v->phase[stop] == nullptr)
         return fail(QEC_ERR_UNSUPPORTED, "bp_decode: no phase-statistics kernel for this code");
+    const int split_opt = split;
     split = !phase && decode_uses_split(variant, stop, split, B) && merge != nullptr;
     if (split) {
         a.merge = merge;
@@ -1816,9 +1911,18 @@ int launch_decode(const void* variant, const Code& c, const uint8_t* sX, const u
     relabel(c.EX.data(), c.J, c.L, c.P, v->relabel, a.SX, a.DX, a.CX);
     relabel(c.EZ.data(), c.K, c.L, c.P, v->relabel, a.SZ, a.DZ, a.CZ);
     const int wavesPerBlock = v->waves_per_block;
+    const bool seq = !phase && !split && decode_uses_seq(v, stop, split_opt);
     const long long waves = (B + a.G - 1) / a.G * (split ? 2 : 1);
     const long long blocks = (waves + wavesPerBlock - 1) / wavesPerBlock;
     if (blocks > 0x7fffffffLL) return fail(QEC_ERR_ARG, "batch too large for one launch");
+    if (seq) {  // sector X, then sector Z (which ORs its flags into X's byte) on the same stream
+        for (int sec = 0; sec < 2; ++sec) {
+            hipLaunchKernelGGL(v->seq[stop][sec], dim3((unsigned)blocks), dim3(64 * wavesPerBlock), 0, stream, a);
+            hipError_t err = hipGetLastError();
+            if (err != hipSuccess) return fail(QEC_ERR_HIP, std::string("bp_decode launch: ") + hipGetErrorString(err));
+        }
+        return QEC_OK;
+    }
     hipLaunchKernelGGL(phase ? v->phase[stop] : split ? v->split[stop] : v->fn[stop], dim3((unsigned)blocks),
                        dim3(64 * wavesPerBlock), 0, stream, a);
     hipError_t err = hipGetLastError();
@@ -1827,6 +1931,21 @@ int launch_decode(const void* variant, const Code& c, const uint8_t* sX, const u
 }
 
 bool decode_has_list(const void* variant) { return static_cast<const Variant*>(variant)->list != nullptr; }
+
+// Compute units of the current device (4 SIMDs each), cached per device (the list-mode grid).
+static int device_cus()
+{
+    static std::atomic<int> cached[64] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0) dev = 0;
+    if (dev >= 64) dev = 63;
+    int c = cached[dev].load(std::memory_order_relaxed);  // every writer stores the same value
+    if (c <= 0) {
+        if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c <= 0) c = 256;
+        cached[dev].store(c, std::memory_order_relaxed);
+    }
+    return c;
+}
 
 // The iteration-0 pattern masks of both sectors (triage.hip): bit idx of hd = pattern idx decides 1
 // (some table entry >= 0.5f), of cv = its R messages all lie outside (0.01, 0.99) -- the host table's
@@ -1891,7 +2010,7 @@ int launch_decode_list(const void* variant, const Code& c, const uint8_t* sX, co
         const int v = e ? std::atoi(e) : 0;
         return (long long)(v >= 1 && v <= 64 ? v : 1);
     }();
-    const long long cap = 1024LL * v->min_waves_syn * rounds;  // one per resident slot of the chip
+    const long long cap = 4LL * device_cus() * v->min_waves_syn * rounds;  // one per resident slot of the chip
     const long long waves = need < cap ? need : cap;
     const int wpb = v->waves_per_block;
     const long long blocks = (waves + wpb - 1) / wpb;

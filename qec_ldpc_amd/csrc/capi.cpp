@@ -40,6 +40,12 @@ bool decode_has_phase_stats(const void* variant, int stop);
 int launch_sample_depolarizing(uint64_t seed, uint64_t start, long long B, int n, float p, uint8_t* x, uint8_t* z,
                                hipStream_t st);
 int launch_mc_errors_syndrome(int src, const McArgsHost& h, hipStream_t st);
+bool statistics_lane_shape(int estride, int rec_stride);
+bool mc_fused_supported(const Code& c, int rec_stride);
+int launch_mc_fused(const Code& c, uint64_t seed, uint64_t start, long long B, float p, const uint32_t pats[4],
+                    uint32_t* sX, uint32_t* sZ, uint8_t* rec, int rec_stride, int32_t* iters, uint32_t* merge,
+                    int32_t* listX, int32_t* listZ, int32_t* listS, uint32_t* counts, const uint64_t* imp_cols,
+                    unsigned long long* counters, bool survivors, hipStream_t st);
 int launch_statistics_packed(const Code& c, const uint64_t* imp_cols, const uint8_t* errp, int estride, const uint8_t* rec,
                              const int32_t* iters, long long B, unsigned long long* counters, hipStream_t st,
                              int rec_stride = 0);
@@ -82,7 +88,7 @@ struct qec_decoder {
     int hard_paths = 1;             // QEC_OPT_HARD_PATHS
     int cycle_jump = 1;             // QEC_OPT_CYCLE_JUMP
     int schedule = 1;               // QEC_OPT_SCHEDULE (0 off, 1 auto, 2 always, 3 always with the local order)
-    int sector_split = 1;           // QEC_OPT_SECTOR_SPLIT (0 off, 1 auto, 2 on)
+    int sector_split = 1;           // QEC_OPT_SECTOR_SPLIT (0 off, 1 auto, 2 split waves, 3 sector launches)
     int phase_stats = 0;            // QEC_OPT_PHASE_STATS
     int triage = 1;                 // QEC_OPT_TRIAGE
     // workspace shared by every launch of this handle (dispatch order, split-flag merge words,
@@ -90,7 +96,7 @@ struct qec_decoder {
     // on another stream waits for it (stream-ordered reuse)
     DeviceArray<uint8_t> sched;
     DeviceArray<uint32_t> merge;
-    DeviceArray<int32_t> tlist;  // triage: listX [B], listZ [B], counts [2]
+    DeviceArray<int32_t> tlist;  // triage: listX [B], listZ [B], (fused Monte-Carlo: listS [B]), counts
     hipEvent_t ws_ev = nullptr;
     hipStream_t ws_stream = nullptr;
     bool ws_used = false;
@@ -452,7 +458,7 @@ int qec_decoder_set_option(qec_decoder* d, int option, int value)
         d->schedule = value;
         return QEC_OK;
     case QEC_OPT_SECTOR_SPLIT:
-        if (value < 0 || value > 2) return fail(QEC_ERR_ARG, "qec_decoder_set_option: QEC_OPT_SECTOR_SPLIT is 0, 1 or 2");
+        if (value < 0 || value > 3) return fail(QEC_ERR_ARG, "qec_decoder_set_option: QEC_OPT_SECTOR_SPLIT is 0 .. 3");
         d->sector_split = value;
         return QEC_OK;
     case QEC_OPT_PHASE_STATS:
@@ -461,7 +467,7 @@ int qec_decoder_set_option(qec_decoder* d, int option, int value)
         d->phase_stats = value != 0;
         return QEC_OK;
     case QEC_OPT_TRIAGE:
-        if (value < 0 || value > 2) return fail(QEC_ERR_ARG, "qec_decoder_set_option: QEC_OPT_TRIAGE is 0, 1 or 2");
+        if (value < 0 || value > 3) return fail(QEC_ERR_ARG, "qec_decoder_set_option: QEC_OPT_TRIAGE is 0 .. 3");
         d->triage = value;
         return QEC_OK;
     default: return fail(QEC_ERR_ARG, "qec_decoder_set_option: unknown option");
@@ -502,6 +508,17 @@ constexpr long long kScheduleMaxSingle = 1LL << 19;
 constexpr float kScheduleSyndromeMinP = 0.004f;
 constexpr float kTriageMaxP = 0.01f;  // QEC_OPT_TRIAGE = 1 triages syndrome-stop batches up to this p
 
+int hard_path_bits(const qec_decoder* d)
+{
+    return (d->hard_paths ? (QEC_HP_FORMS | (d->cycle_jump ? QEC_HP_CYCLE : 0)) : 0) | (d->phase_stats ? QEC_HP_PHASE : 0);
+}
+
+// QEC_OPT_TRIAGE: 1 (auto) and 3 (auto, never the fused Monte-Carlo kernel) up to kTriageMaxP, 2 always
+bool triage_on(const qec_decoder* d, float p)
+{
+    return !d->phase_stats && (d->triage == 2 || ((d->triage == 1 || d->triage == 3) && p <= kTriageMaxP));
+}
+
 // One decode launch of a single-device handle on device buffers.  Outputs: byte form (eX, eZ,
 // flags) or, with rec non-null, the packed decision records.
 // sbits: sX / sZ are bit rows ([B][ceil(m/32)] words, the Monte-Carlo pipeline's layout; wave-circulant
@@ -531,8 +548,7 @@ int dispatch_decode(qec_decoder* d, const uint8_t* sX, const uint8_t* sZ, long l
         if (rc) return rc;
         return ws_release(d, st);
     }
-    const int hp = (d->hard_paths ? (QEC_HP_FORMS | (d->cycle_jump ? QEC_HP_CYCLE : 0)) : 0) |
-                   (d->phase_stats ? QEC_HP_PHASE : 0);
+    const int hp = hard_path_bits(d);
     // syndrome stop on bit rows into records (the Monte-Carlo pipeline): triage iteration 0 for 64
     // syndromes per wave, then decode only the sectors it passes on (triage.hip, list mode)
     // Above p = 0.01 most sectors go on past iteration 0 (P61 at p = 0.02: 2.2 iterations per sector)
@@ -540,9 +556,9 @@ int dispatch_decode(qec_decoder* d, const uint8_t* sX, const uint8_t* sZ, long l
     // launch (140 vs 178 M syn/s at p = 0.02, 6.4 vs 8.3 at 0.1; 1.47 G vs 0.50 G at 0.002,
     // profiles/r03/psweep_triage.json), so the triage stays off there.
     uint32_t pats[4];
-    if (d->triage && !d->phase_stats && stop == QEC_STOP_SYNDROME && sbits && rec != nullptr && q == nullptr &&
-        (d->triage == 2 || p <= kTriageMaxP) &&
+    if (triage_on(d, p) && stop == QEC_STOP_SYNDROME && sbits && rec != nullptr && q == nullptr &&
         maxIter >= 2 && B < (1LL << 31) && decode_has_list(d->variant) && triage_supported(c) && triage_aligned(sX, sZ) &&
+        (reinterpret_cast<uintptr_t>(iters) & 7u) == 0 &&  // the triage stores both counts as one 8-byte word
         decode_pattern_masks(d->variant, p, pats)) {
         if ((rc = ws_reserve(d->merge, (size_t)B, st, "decode")) || (rc = ws_reserve(d->tlist, 2 * (size_t)B + 2, st, "decode")))
             return rc;
@@ -790,6 +806,43 @@ int mc_batch(qec_decoder* d, McArgsHost h, int src, float p, int maxIter, int st
     // the depolarising front end hands the wave-circulant engine its syndromes as bit rows and its
     // packed errors at word-aligned rows (72 + 156 instead of 549 + 154 B per P61 sample)
     const bool bits = src == MC_SRC_PHILOX && d->engine != QEC_ENGINE_SPARSE;
+    const int nb = (c.n + 7) / 8;
+    const int estride = bits ? 4 * ((2 * nb + 3) / 4) : 2 * nb;
+    const int padded = 4 * ((2 * nb + 1 + 3) / 4);
+    const int rstride = bits && statistics_lane_shape(estride, padded) ? padded : 2 * nb + 1;
+    // the fused low-p pipeline (triage.hip: sampler, syndromes, iteration-0 triage and the finished
+    // samples' statistics in one kernel; the list-mode decode and the survivors' statistics after it)
+    uint32_t pats[4];
+    if (bits && stop == QEC_STOP_SYNDROME && want_iters && d->triage != 3 && triage_on(d, p) && maxIter >= 2 &&
+        h.B < (1LL << 31) && decode_has_list(d->variant) && mc_fused_supported(c, rstride) &&
+        decode_pattern_masks(d->variant, p, pats)) {
+        const long long B = h.B;
+        int rc = ws_acquire(d, st);
+        if (rc) return rc;
+        if ((rc = ws_reserve(d->merge, (size_t)B, st, "monte carlo")) ||
+            (rc = ws_reserve(d->tlist, 3 * (size_t)B + 3, st, "monte carlo")))
+            return rc;
+        int32_t* lX = d->tlist.data();
+        int32_t* lZ = lX + B;
+        int32_t* lS = lZ + B;
+        uint32_t* cnt = reinterpret_cast<uint32_t*>(lS + B);
+        uint32_t* sXp = reinterpret_cast<uint32_t*>(d->msX.data());
+        uint32_t* sZp = reinterpret_cast<uint32_t*>(d->msZ.data());
+        QEC_HIP_CHECK(hipMemsetAsync(cnt, 0, 3 * sizeof(uint32_t), st));
+        if (ev0) QEC_HIP_CHECK(hipEventRecord(ev0, st));
+        for (int pass = 0; pass < 2; ++pass) {
+            if (pass == 1) {
+                rc = launch_decode_list(d->variant, c, d->msX.data(), d->msZ.data(), B, p, maxIter, hard_path_bits(d),
+                                        d->mrec.data(), d->mit.data(), d->merge.data(), lX, lZ, cnt, st, rstride);
+                if (rc) return rc;
+                if (ev1) QEC_HIP_CHECK(hipEventRecord(ev1, st));
+            }
+            rc = launch_mc_fused(c, h.seed, h.start, B, h.p, pats, sXp, sZp, d->mrec.data(), rstride, d->mit.data(),
+                                 d->merge.data(), lX, lZ, lS, cnt, d->imp_cols.data(), d->mcount.data(), pass == 1, st);
+            if (rc) return rc;
+        }
+        return ws_release(d, st);
+    }
     if (bits) {
         h.sXp = reinterpret_cast<uint32_t*>(d->msX.data());
         h.sZp = reinterpret_cast<uint32_t*>(d->msZ.data());
@@ -801,17 +854,16 @@ int mc_batch(qec_decoder* d, McArgsHost h, int src, float p, int maxIter, int st
     int rc = launch_mc_errors_syndrome(src, h, st);
     if (rc) return rc;
     if (ev0) QEC_HIP_CHECK(hipEventRecord(ev0, st));
-    // records at word-aligned rows (156 instead of 155 B for P61) on the bit-row path: the statistics
-    // kernel then reads both its arrays a word at a time
-    const int nb = (c.n + 7) / 8;
-    const int rstride = bits ? 4 * ((2 * nb + 1 + 3) / 4) : 2 * nb + 1;
+    // records at word-aligned rows (156 instead of 155 B for P61) on the bit-row path where the lane
+    // statistics kernel has that row shape (rstride above: it then reads both arrays a word at a time);
+    // every other code keeps the public 2 nb + 1 rows, which the other statistics kernel, the triage
+    // and the list-mode decode take as they are
     rc = dispatch_decode(d, d->msX.data(), d->msZ.data(), h.B, p, maxIter, stop, nullptr, nullptr, nullptr,
                          d->mrec.data(), want_iters ? d->mit.data() : nullptr, nullptr, st, bits, rstride);
     if (rc) return rc;
     if (ev1) QEC_HIP_CHECK(hipEventRecord(ev1, st));
-    return launch_statistics_packed(c, d->imp_cols.data(), d->merrp.data(), bits ? 4 * ((2 * nb + 3) / 4) : 2 * nb,
-                                    d->mrec.data(), want_iters ? d->mit.data() : nullptr, h.B, d->mcount.data(), st,
-                                    rstride);
+    return launch_statistics_packed(c, d->imp_cols.data(), d->merrp.data(), estride, d->mrec.data(),
+                                    want_iters ? d->mit.data() : nullptr, h.B, d->mcount.data(), st, rstride);
 }
 
 int mc_fetch_counters(qec_decoder* d, unsigned long long* out)

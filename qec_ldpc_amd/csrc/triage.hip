@@ -18,28 +18,39 @@
 // decode kernel produces for it (tests/test_gpu_triage.py checks that bit for bit).  The others are
 // appended to per-sector lists that the decode kernel's list mode then decodes from scratch; the two
 // sectors of a syndrome meet in its merge word as in the sector-split launches (done bit + flags).
+//
+// The fused Monte-Carlo form (mc_fused_kernel, qec_monte_carlo at low p): sampler -> syndrome bits in
+// LDS -> this triage -> residual against the sample's hits -> I-P check -> counters, in one kernel; only
+// the samples with a sector that goes on (about 1 % of P61 samples at p = 0.002) reach HBM, for the
+// list-mode decode and the survivor statistics (mc_survivor_kernel, which walks the sample again).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 #include <cstdlib>
 
 #include "qec_device.h"
 #include "qec_internal.h"
+#include "qec_mc.h"
 
 namespace qec {
 
 constexpr int kTriageWaves = 4;
+
+struct TriageMasks {
+    uint32_t hdpatX, cvpatX, hdpatZ, cvpatZ;  // bit idx: pattern idx decides 1 / stays outside (0.01, 0.99)
+    // the same masks by count when they depend only on the number of unsatisfied checks (symmetric):
+    // bit c = the value for patterns with c ones; sym* = 0 when a mask is not symmetric (pattern trees)
+    uint32_t hdcntX, cvcntX, hdcntZ, cvcntZ;
+    int symX, symZ;
+};
 
 struct TriageArgs {
     const uint32_t* sX;  // [B][wX] bit rows (bit c = check c)
     const uint32_t* sZ;  // [B][wZ]
     long long B;
     int wX, wZ, nb, recB;  // recB: record row stride (>= 2 nb + 1)
-    uint32_t hdpatX, cvpatX, hdpatZ, cvpatZ;  // bit idx: pattern idx decides 1 / stays outside (0.01, 0.99)
-    // the same masks by count when they depend only on the number of unsatisfied checks (symmetric):
-    // bit c = the value for patterns with c ones; sym* = 0 when a mask is not symmetric (pattern trees)
-    uint32_t hdcntX, cvcntX, hdcntZ, cvcntZ;
-    int symX, symZ;
+    TriageMasks m;
     uint8_t* rec;        // [B][recB] decision records
     int32_t* iters;      // [B][2] or null
     uint32_t* merge;     // [B]: done bit (0x100 X, 0x200 Z) + that sector's flags
@@ -119,21 +130,16 @@ __device__ __forceinline__ void count_ones(const uint64_t (&v)[R], uint64_t (&b)
 // whether iteration 0 satisfies the syndrome, and whether some message lies inside (0.01, 0.99).
 // SYM: the masks are symmetric (hdcnt / cvcnt by count of ones): an adder tree and a 3-level
 // multiplexer instead of the 2^R-leaf trees (P61 Z: 16 instead of 124 bit operations per block).
-template <int R, int L, int P, class EXP, int SEC, bool SYM>
-__device__ __forceinline__ bool triage_sector(const uint32_t* __restrict__ rows, long long b, uint32_t hdpat,
-                                              uint32_t cvpat, uint32_t hdcnt, uint32_t cvcnt, uint64_t (&hd)[L],
-                                              bool& cvbad)
+// words of a sector's syndrome bit row (R P bits)
+template <int R, int P>
+constexpr int row_words() { return (R * P + 31) / 32; }
+
+// The bit row of syndrome b, kW words at a compile-time stride from a 16-byte aligned base
+// (launch_triage checks): 16- or 8-byte loads where the row's alignment allows (P61: X 2 x 16 B, Z
+// 5 x 8 B instead of 18 dword loads per lane); w[kW], w[kW + 1] = 0.
+template <int kW>
+__device__ __forceinline__ void load_row(const uint32_t* __restrict__ rows, long long b, uint32_t (&w)[kW + 2])
 {
-    static_assert(R <= 5 && P <= 64, "patterns in 32 bits, blocks in 64");
-    constexpr EXP tab = EXP::make();
-    auto E = [&](int r, int l) constexpr { return SEC ? tab.EZ[r][l] : tab.EX[r][l]; };
-    constexpr uint64_t mask = P >= 64 ? ~0ull : (1ull << P) - 1ull;
-    constexpr int kW = (R * P + 31) / 32;  // words of the row
-    constexpr uint32_t full = R >= 5 ? 0xFFFFFFFFu : (1u << (1 << R)) - 1u;
-    uint32_t w[kW + 2];
-    // the row, kW words at a compile-time stride from a 16-byte aligned base (launch_triage checks):
-    // 16- or 8-byte loads where the row's alignment allows (P61: X 2 x 16 B, Z 5 x 8 B instead of 18
-    // dword loads per lane)
     const uint32_t* __restrict__ row = rows + b * kW;
     if constexpr (kW % 4 == 0) {
 #pragma unroll
@@ -153,6 +159,18 @@ __device__ __forceinline__ bool triage_sector(const uint32_t* __restrict__ rows,
     }
     w[kW] = 0u;
     w[kW + 1] = 0u;
+}
+
+template <int R, int L, int P, class EXP, int SEC, bool SYM>
+__device__ __forceinline__ bool triage_sector(const uint32_t (&w)[row_words<R, P>() + 2], uint32_t hdpat,
+                                              uint32_t cvpat, uint32_t hdcnt, uint32_t cvcnt, uint64_t (&hd)[L],
+                                              bool& cvbad)
+{
+    static_assert(R <= 5 && P <= 64, "patterns in 32 bits, blocks in 64");
+    constexpr EXP tab = EXP::make();
+    auto E = [&](int r, int l) constexpr { return SEC ? tab.EZ[r][l] : tab.EX[r][l]; };
+    constexpr uint64_t mask = P >= 64 ? ~0ull : (1ull << P) - 1ull;
+    constexpr uint32_t full = R >= 5 ? 0xFFFFFFFFu : (uint32_t)((1ull << (1 << R)) - 1ull);
     uint64_t s[R];  // block row r: bit i = check (r, i)
 #pragma unroll
     for (int r = 0; r < R; ++r) {
@@ -245,6 +263,23 @@ __device__ __forceinline__ void stage_record_dw(uint32_t* __restrict__ row, int 
     for (int d = nrec; d < ndw; ++d) row[d] = 0u;  // row padding
 }
 
+// Both sectors of one syndrome: symmetric masks (the usual case) take the adder form; R <= 3 gains
+// nothing from it.
+template <int J, int K, int L, int P, class EXP>
+__device__ __forceinline__ void triage_both(const TriageMasks& m, const uint32_t (&wX)[row_words<J, P>() + 2],
+                                            const uint32_t (&wZ)[row_words<K, P>() + 2], uint64_t (&hdX)[L],
+                                            uint64_t (&hdZ)[L], bool& cvbX, bool& cvbZ, bool& okX, bool& okZ)
+{
+    if (J >= 4 && m.symX)
+        okX = triage_sector<J, L, P, EXP, 0, J >= 4>(wX, m.hdpatX, m.cvpatX, m.hdcntX, m.cvcntX, hdX, cvbX);
+    else
+        okX = triage_sector<J, L, P, EXP, 0, false>(wX, m.hdpatX, m.cvpatX, 0u, 0u, hdX, cvbX);
+    if (K >= 4 && m.symZ)
+        okZ = triage_sector<K, L, P, EXP, 1, K >= 4>(wZ, m.hdpatZ, m.cvpatZ, m.hdcntZ, m.cvcntZ, hdZ, cvbZ);
+    else
+        okZ = triage_sector<K, L, P, EXP, 1, false>(wZ, m.hdpatZ, m.cvpatZ, 0u, 0u, hdZ, cvbZ);
+}
+
 template <int J, int K, int L, int P, int S, int T>
 __global__ __launch_bounds__(64 * kTriageWaves) void triage_kernel(const TriageArgs a)
 {
@@ -262,16 +297,11 @@ __global__ __launch_bounds__(64 * kTriageWaves) void triage_kernel(const TriageA
     uint64_t hdX[L], hdZ[L];
     bool cvbX = false, cvbZ = false;
     using EXP = QcExponents<J, K, L, P, S, T>;
-    // symmetric masks (the usual case) take the adder form; R <= 3 gains nothing from it
+    uint32_t wX[row_words<J, P>() + 2], wZ[row_words<K, P>() + 2];
+    load_row<row_words<J, P>()>(a.sX, bl, wX);
+    load_row<row_words<K, P>()>(a.sZ, bl, wZ);
     bool okX, okZ;
-    if (J >= 4 && a.symX)
-        okX = triage_sector<J, L, P, EXP, 0, J >= 4>(a.sX, bl, a.hdpatX, a.cvpatX, a.hdcntX, a.cvcntX, hdX, cvbX);
-    else
-        okX = triage_sector<J, L, P, EXP, 0, false>(a.sX, bl, a.hdpatX, a.cvpatX, 0u, 0u, hdX, cvbX);
-    if (K >= 4 && a.symZ)
-        okZ = triage_sector<K, L, P, EXP, 1, K >= 4>(a.sZ, bl, a.hdpatZ, a.cvpatZ, a.hdcntZ, a.cvcntZ, hdZ, cvbZ);
-    else
-        okZ = triage_sector<K, L, P, EXP, 1, false>(a.sZ, bl, a.hdpatZ, a.cvpatZ, 0u, 0u, hdZ, cvbZ);
+    triage_both<J, K, L, P, EXP>(a.m, wX, wZ, hdX, hdZ, cvbX, cvbZ, okX, okZ);
     const bool doneX = valid && okX, doneZ = valid && okZ;
     const uint32_t fX = cvbX ? QEC_CONVERGENCE_FAIL_X : 0u, fZ = cvbZ ? QEC_CONVERGENCE_FAIL_Z : 0u;
     // record rows: both sectors' decisions (a sector that goes on is overwritten by the list decode),
@@ -337,6 +367,310 @@ __global__ __launch_bounds__(64 * kTriageWaves) void triage_kernel(const TriageA
     if ((gz >> lane) & 1ull) a.listZ[baseZ + __popcll(gz & lt)] = (int32_t)b;
 }
 
+// ---- fused low-p Monte-Carlo pipeline ---------------------------------------------------------
+// One lane per sample, 64 samples per wave (DecoderCPU.h:438-521 for each, batched):
+//   1. the gap walk (qec_mc.h) of sample start + b: every hit flips its qubit's checks in the lane's
+//      syndrome bit rows in LDS (as mc_gap_kernel) and is kept in the lane's hit list (qubit << 2 | type,
+//      up to kHitCap of them);
+//   2. the iteration-0 triage of both sectors on those rows (triage_both);
+//   3. a sample whose two sectors stop there and whose hits fit the list is finished here: its decision
+//      equals its error iff every hit qubit is decided in its sector(s) and nothing else is (counts of
+//      set bits), else the residual goes through the I-P columns (logical_from_columns), and the
+//      CodeStatistics counters (DecoderCPU.h:464-521) are counted with iterations 1 + 1;
+//   4. any other sample (a sector goes on, or more hits than the list holds) is a survivor: its
+//      syndrome rows, its record with the triage's decisions, its iteration counts and merge word are
+//      written as the triage kernel writes them, it is appended to listX / listZ for the sectors that
+//      go on and to listS, and mc_survivor_kernel counts it after the list-mode decode.
+// withX / withZ (errors present) are counted here for every sample.
+constexpr int kFusedWaves = 4;
+constexpr int kHitCap = 16;  // hits a lane keeps (P61 at p = 0.01: 6.1 on average)
+
+struct FusedArgs {
+    GapParams gp;
+    uint64_t start;  // sample index of batch row 0
+    long long B;
+    int recB;        // record row stride (a multiple of 4)
+    TriageMasks m;
+    uint32_t* sX;    // [B][wX] bit rows (survivors only)
+    uint32_t* sZ;
+    uint8_t* rec;    // [B][recB] (survivors only)
+    int32_t* iters;  // [B][2] (survivors only)
+    uint32_t* merge; // [B] (survivors only)
+    int32_t* listX;
+    int32_t* listZ;
+    int32_t* listS;
+    uint32_t* counts;  // [3]: listX, listZ, listS lengths (zeroed before the launch)
+    const uint64_t* imp_cols;
+    int imp_cw;
+    unsigned long long* counters;  // [C_N + 2] (iteration sums at C_N, C_N + 1)
+};
+
+// Decision bits of this lane's sample in the record layout (x bits at [0, 8 nb), z at [8 nb, 16 nb)), as
+// u32 words [0, 2 NW) with the flags byte left 0, XOR its hits: the residual the I-P check takes.
+template <int L, int P, int NW>
+__device__ __forceinline__ void residual_words(uint32_t* __restrict__ out, const uint64_t (&hdX)[L], const uint64_t (&hdZ)[L],
+                                               const uint16_t* __restrict__ hits, int nh)
+{
+    constexpr int nb = (L * P + 7) / 8;
+    stage_record_dw<L, P>(out, 2 * NW, hdX, hdZ, 0u);
+    for (int h = 0; h < nh; ++h) {
+        const int v = hits[h] >> 2, t = hits[h] & 3;
+        if (t != 2) out[v >> 5] ^= 1u << (v & 31);
+        if (t != 0) out[(8 * nb + v) >> 5] ^= 1u << ((8 * nb + v) & 31);
+    }
+}
+
+// the wave's counters (ballot popcounts, iteration sums) added to the global ones once per workgroup
+template <int NWAVES>
+__device__ __forceinline__ void flush_counters(const unsigned long long (&c)[C_N + 2], unsigned long long (*part)[C_N + 2],
+                                               unsigned long long* __restrict__ counters)
+{
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    if (lane < C_N + 2) {
+        unsigned long long v = 0;
+#pragma unroll
+        for (int k = 0; k < C_N + 2; ++k) v = lane == k ? c[k] : v;
+        part[wv][lane] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < C_N + 2) {
+        unsigned long long v = 0;
+        for (int w = 0; w < NWAVES; ++w) v += part[w][threadIdx.x];
+        if (v) atomicAdd(&counters[threadIdx.x], v);
+    }
+}
+
+template <int J, int K, int L, int P, int S, int T_>
+__global__ __launch_bounds__(64 * kFusedWaves) void mc_fused_kernel(const FusedArgs a)
+{
+    using EXP = QcExponents<J, K, L, P, S, T_>;
+    constexpr EXP tab = EXP::make();
+    constexpr int n = L * P, nb = (n + 7) / 8;
+    constexpr int kWX = row_words<J, P>(), kWZ = row_words<K, P>();
+    constexpr int RS = (kWX + kWZ + kHitCap / 2) | 1;  // lane region (odd: the lanes' words in distinct banks)
+    constexpr int NW = (2 * nb + 7) / 8;                // 64-bit residual words (record layout)
+    __shared__ uint32_t T[n + 1];
+    __shared__ int E[(J + K) * L];
+    __shared__ uint32_t region[64 * kFusedWaves * RS];
+    __shared__ unsigned long long sres[kFusedWaves][NW];
+    __shared__ unsigned long long part[kFusedWaves][C_N + 2];
+    __shared__ uint32_t wcnt[kFusedWaves][3], wgbase[3];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    gap_table(a.gp, n, T);
+    for (int t = threadIdx.x; t < (J + K) * L; t += blockDim.x)
+        E[t] = t < J * L ? tab.EX[t / L][t % L] : tab.EZ[(t - J * L) / L][(t - J * L) % L];
+    uint32_t* __restrict__ mine = region + threadIdx.x * RS;
+    for (int k = 0; k < RS; ++k) mine[k] = 0u;
+    __syncthreads();
+    const long long b0 = ((long long)blockIdx.x * kFusedWaves + wv) * 64;
+    const long long b = b0 + lane;
+    const bool valid = b < a.B;
+    uint32_t* __restrict__ synX = mine;
+    uint32_t* __restrict__ synZ = mine + kWX;
+    uint16_t* __restrict__ hits = reinterpret_cast<uint16_t*>(mine + kWX + kWZ);
+    int nh = 0;
+    bool anyX = false, anyZ = false;
+    if (valid && a.gp.thr != 0) {
+        gap_walk(a.gp, a.start + (uint64_t)b, n, T, [&](int v, uint32_t t) {
+            const bool ex = t != 2, ez = t != 0;
+            anyX |= ex;
+            anyZ |= ez;
+            if (nh < kHitCap) hits[nh] = (uint16_t)(v << 2 | (int)t);
+            ++nh;
+            // qubit (l, j) sits in check (r, (j - E[r][l]) mod P) of each block row r
+            const int l = v / P, j = v - l * P;
+            if (ex)
+#pragma unroll
+                for (int r = 0; r < J; ++r) {
+                    const int d = j - E[r * L + l];
+                    const int c = r * P + (d < 0 ? d + P : d);
+                    atomicXor(&synX[c >> 5], 1u << (c & 31));
+                }
+            if (ez)
+#pragma unroll
+                for (int r = 0; r < K; ++r) {
+                    const int d = j - E[(J + r) * L + l];
+                    const int c = r * P + (d < 0 ? d + P : d);
+                    atomicXor(&synZ[c >> 5], 1u << (c & 31));
+                }
+        });
+    }
+    uint32_t wX[kWX + 2], wZ[kWZ + 2];
+#pragma unroll
+    for (int k = 0; k < kWX; ++k) wX[k] = synX[k];
+#pragma unroll
+    for (int k = 0; k < kWZ; ++k) wZ[k] = synZ[k];
+    wX[kWX] = wX[kWX + 1] = wZ[kWZ] = wZ[kWZ + 1] = 0u;
+    uint64_t hdX[L], hdZ[L];
+    bool cvbX = false, cvbZ = false, okX, okZ;
+    triage_both<J, K, L, P, EXP>(a.m, wX, wZ, hdX, hdZ, cvbX, cvbZ, okX, okZ);
+    const uint32_t fX = cvbX ? QEC_CONVERGENCE_FAIL_X : 0u, fZ = cvbZ ? QEC_CONVERGENCE_FAIL_Z : 0u;
+    const bool done = valid && okX && okZ && nh <= kHitCap;
+    const bool surv = valid && !done;
+    // a finished sample's decision equals its error iff each hit qubit is decided in its sector(s) and
+    // the decisions hold no other bit (the walk hits a qubit at most once)
+    bool match = true;
+    if (done) {
+        int cx = 0, cz = 0, hx = 0, hz = 0;
+#pragma unroll
+        for (int l = 0; l < L; ++l) { cx += __popcll(hdX[l]); cz += __popcll(hdZ[l]); }
+        for (int h = 0; h < nh; ++h) {
+            const int v = hits[h] >> 2, t = hits[h] & 3;
+            const int l = v / P, j = v - l * P;
+            uint64_t x = 0, z = 0;
+#pragma unroll
+            for (int q = 0; q < L; ++q) {  // select, not a dynamic register index
+                x = q == l ? hdX[q] : x;
+                z = q == l ? hdZ[q] : z;
+            }
+            if (t != 2) { match &= ((x >> j) & 1ull) != 0ull; ++hx; }
+            if (t != 0) { match &= ((z >> j) & 1ull) != 0ull; ++hz; }
+        }
+        match &= cx == hx && cz == hz;
+    }
+    // the rare finished sample whose decision differs from its error: the I-P check, one at a time
+    unsigned long long need = __ballot(done && !match), logical = 0;
+    while (need) {
+        const int sl = __builtin_ctzll(need);
+        need &= need - 1;
+        if (lane == sl) residual_words<L, P, NW>(reinterpret_cast<uint32_t*>(sres[wv]), hdX, hdZ, hits, nh);
+        wave_sync();
+        if (logical_from_columns<true>(sres[wv], NW, n, nb, a.imp_cols, a.imp_cw, lane)) logical |= 1ull << sl;
+        wave_sync();
+    }
+    // survivors: what the triage kernel writes for a syndrome, and the lists
+    if (surv) {
+#pragma unroll
+        for (int k = 0; k < kWX; ++k) a.sX[b * kWX + k] = wX[k];
+#pragma unroll
+        for (int k = 0; k < kWZ; ++k) a.sZ[b * kWZ + k] = wZ[k];
+        stage_record_dw<L, P>(reinterpret_cast<uint32_t*>(a.rec + b * a.recB), a.recB >> 2, hdX, hdZ, fX | fZ);
+        *reinterpret_cast<int2*>(a.iters + 2 * b) = make_int2(1, 1);  // list sectors rewrite theirs
+        a.merge[b] = (okX ? 0x100u | fX : 0u) | (okZ ? 0x200u | fZ : 0u);
+    }
+    const unsigned long long gx = __ballot(surv && !okX), gz = __ballot(surv && !okZ), gs = __ballot(surv);
+    const unsigned long long dm = __ballot(done);
+    unsigned long long c[C_N + 2] = {};
+    c[C_WITHX] = __popcll(__ballot(valid && anyX));
+    c[C_WITHZ] = __popcll(__ballot(valid && anyZ));
+    c[C_LOGICAL] = __popcll(dm & logical);
+    c[C_CORRECTED] = __popcll(dm & ~logical);
+    c[C_CONVX] = __popcll(__ballot(done && cvbX));
+    c[C_CONVZ] = __popcll(__ballot(done && cvbZ));
+    c[C_N] = c[C_N + 1] = __popcll(dm);  // one iteration per sector
+    // list appends: one atomic per workgroup and list (same-address atomics serialise at L2)
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    if (lane == 0) {
+        wcnt[wv][0] = (uint32_t)__popcll(gx);
+        wcnt[wv][1] = (uint32_t)__popcll(gz);
+        wcnt[wv][2] = (uint32_t)__popcll(gs);
+    }
+    __syncthreads();
+    if (threadIdx.x < 3) {
+        uint32_t tot = 0;
+        for (int w = 0; w < kFusedWaves; ++w) tot += wcnt[w][threadIdx.x];
+        wgbase[threadIdx.x] = tot ? atomicAdd(&a.counts[threadIdx.x], tot) : 0u;
+    }
+    __syncthreads();
+    uint32_t base[3] = {wgbase[0], wgbase[1], wgbase[2]};
+    for (int w = 0; w < wv; ++w)
+        for (int k = 0; k < 3; ++k) base[k] += wcnt[w][k];
+    if ((gx >> lane) & 1ull) a.listX[base[0] + __popcll(gx & lt)] = (int32_t)b;
+    if ((gz >> lane) & 1ull) a.listZ[base[1] + __popcll(gz & lt)] = (int32_t)b;
+    if ((gs >> lane) & 1ull) a.listS[base[2] + __popcll(gs & lt)] = (int32_t)b;
+    flush_counters<kFusedWaves>(c, part, a.counters);
+}
+
+// The survivors' counters after the list-mode decode: lane per listed sample (grid-stride over
+// listS [0, counts[2])); the sample's errors are walked again into the lane's LDS region in the record
+// layout, XORed with its record (the final decisions), and counted as statistics_lane_kernel counts
+// a sample (syndrome fails from the flags byte, the I-P check when neither failed and the residual is
+// nonzero, convergence fails, both iteration counts).  withX / withZ were counted by mc_fused_kernel.
+constexpr int kSurvWaves = 4;
+
+template <int L, int P>
+__global__ __launch_bounds__(64 * kSurvWaves) void mc_survivor_kernel(const FusedArgs a)
+{
+    constexpr int n = L * P, nb = (n + 7) / 8;
+    constexpr int NW = (2 * nb + 7) / 8;
+    constexpr int RS = (2 * NW) | 1;  // lane region in u32 words (odd stride)
+    __shared__ uint32_t T[n + 1];
+    __shared__ uint32_t region[64 * kSurvWaves * RS];
+    __shared__ unsigned long long sres[kSurvWaves][NW];
+    __shared__ unsigned long long part[kSurvWaves][C_N + 2];
+    const long long cnt = a.counts[2];
+    if ((long long)blockIdx.x * blockDim.x >= cnt) return;  // workgroup-uniform: no survivor for this one
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    gap_table(a.gp, n, T);
+    __syncthreads();
+    uint32_t* __restrict__ mine = region + threadIdx.x * RS;
+    unsigned long long c[C_N + 2] = {};
+    const long long step = (long long)gridDim.x * blockDim.x;
+    for (long long i0 = (long long)blockIdx.x * blockDim.x + wv * 64; i0 < cnt; i0 += step) {
+        const long long idx = i0 + lane;
+        const bool valid = idx < cnt;
+        const long long b = valid ? a.listS[idx] : 0;
+        for (int k = 0; k < RS; ++k) mine[k] = 0u;
+        if (valid && a.gp.thr != 0) {
+            gap_walk(a.gp, a.start + (uint64_t)b, n, T, [&](int v, uint32_t t) {
+                if (t != 2) mine[v >> 5] |= 1u << (v & 31);
+                if (t != 0) mine[(8 * nb + v) >> 5] |= 1u << ((8 * nb + v) & 31);
+            });
+        }
+        // residual = errors ^ decisions over the record's 2 nb decision bytes
+        const uint32_t* __restrict__ r = reinterpret_cast<const uint32_t*>(a.rec + b * a.recB);
+        constexpr int kRW = (2 * nb + 1 + 3) / 4;  // record words holding decisions and the flags byte
+        static_assert(kRW <= 2 * NW, "the lane region holds the record's words");
+        uint32_t nz = 0, f = 0;
+#pragma unroll
+        for (int k = 0; k < kRW; ++k) {
+            const uint32_t rv = valid ? r[k] : 0u;
+            const int rem = 2 * nb - 4 * k;  // decision bytes in word k
+            const uint32_t m = rem >= 4 ? ~0u : rem <= 0 ? 0u : (1u << (8 * rem)) - 1u;
+            if (k == (2 * nb) / 4) f = (rv >> (8 * ((2 * nb) % 4))) & 0xFFu;
+            const uint32_t res = (mine[k] ^ rv) & m;
+            mine[k] = res;
+            nz |= res;
+        }
+        f = valid ? f : 0u;
+        const bool sx = (f & QEC_SYNDROME_FAIL_X) != 0, sz = (f & QEC_SYNDROME_FAIL_Z) != 0;
+        unsigned long long need = __ballot(valid && !(sx || sz) && nz != 0u), logical = 0;
+        while (need) {
+            const int sl = __builtin_ctzll(need);
+            need &= need - 1;
+            if (lane < NW) {
+                const uint32_t* src = region + (wv * 64 + sl) * RS;
+                sres[wv][lane] = (unsigned long long)src[2 * lane] | ((unsigned long long)src[2 * lane + 1] << 32);
+            }
+            wave_sync();
+            if (logical_from_columns<true>(sres[wv], NW, n, nb, a.imp_cols, a.imp_cw, lane)) logical |= 1ull << sl;
+            wave_sync();
+        }
+        const unsigned long long vm = __ballot(valid), bx = __ballot(sx), bz = __ballot(sz);
+        const unsigned long long ok = vm & ~(bx | bz);
+        c[C_SYNX] += __popcll(bx);
+        c[C_SYNZ] += __popcll(bz);
+        c[C_LOGICAL] += __popcll(ok & logical);
+        c[C_CORRECTED] += __popcll(ok & ~logical);
+        c[C_CONVX] += __popcll(__ballot((f & QEC_CONVERGENCE_FAIL_X) != 0));
+        c[C_CONVZ] += __popcll(__ballot((f & QEC_CONVERGENCE_FAIL_Z) != 0));
+        unsigned long long itx = 0, itz = 0;
+        if (valid) {
+            const int2 it = *reinterpret_cast<const int2*>(a.iters + 2 * b);
+            itx = (unsigned)it.x;
+            itz = (unsigned)it.y;
+        }
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) {
+            itx += __shfl_xor(itx, o);
+            itz += __shfl_xor(itz, o);
+        }
+        c[C_N] += itx;
+        c[C_N + 1] += itz;
+    }
+    flush_counters<kSurvWaves>(c, part, a.counters);
+}
+
 using TriageFn = void (*)(const TriageArgs);
 
 // the shipped codes, when the file's tables are its header's generator output (as bp_decode.hip's
@@ -353,12 +687,6 @@ static TriageFn triage_fn(const Code& c)
 }
 
 bool triage_supported(const Code& c) { return c.is_qc && triage_fn(c) != nullptr; }
-
-// the kernel loads rows with 16- / 8-byte loads (triage_sector)
-bool triage_aligned(const void* sX, const void* sZ)
-{
-    return ((reinterpret_cast<uintptr_t>(sX) | reinterpret_cast<uintptr_t>(sZ)) & 15u) == 0;
-}
 
 // pat (bit idx = value for pattern idx of R bits) as a function of the pattern's count of ones: out
 // bit c = the value at count c (counts above R: 0); false if two patterns with one count differ
@@ -379,6 +707,76 @@ static bool by_count(uint32_t pat, int R, uint32_t& out)
     return true;
 }
 
+static TriageMasks triage_masks(const Code& c, const uint32_t pats[4])
+{
+    TriageMasks m{};
+    m.hdpatX = pats[0]; m.cvpatX = pats[1]; m.hdpatZ = pats[2]; m.cvpatZ = pats[3];
+    m.symX = by_count(pats[0], c.J, m.hdcntX) && by_count(pats[1], c.J, m.cvcntX);
+    m.symZ = by_count(pats[2], c.K, m.hdcntZ) && by_count(pats[3], c.K, m.cvcntZ);
+    const char* trees = std::getenv("QEC_TRIAGE_TREES");  // tests: force the pattern-tree form
+    if (trees && trees[0] == '1') m.symX = m.symZ = 0;
+    return m;
+}
+
+using FusedFn = void (*)(const FusedArgs);
+
+// the fused kernels of the shipped codes (as triage_fn)
+static bool fused_fns(const Code& c, FusedFn& fused, FusedFn& surv)
+{
+    if (!triage_supported(c)) return false;
+    if (c.P == 61) { fused = mc_fused_kernel<4, 5, 10, 61, 9, 49>; surv = mc_survivor_kernel<10, 61>; }
+    else { fused = mc_fused_kernel<3, 3, 6, 7, 2, 3>; surv = mc_survivor_kernel<6, 7>; }
+    return true;
+}
+
+bool mc_fused_supported(const Code& c, int rec_stride)
+{
+    FusedFn f, s;
+    return fused_fns(c, f, s) && rec_stride % 4 == 0 && rec_stride >= 2 * ((c.n + 7) / 8) + 1 &&
+           c.imp_col_words <= 64 && 2 * c.n < (1 << 14);
+}
+
+// The fused pipeline's first kernel (sample, syndromes, triage, finished samples' statistics) and,
+// after the caller's list-mode decode, the survivors' statistics.  counts[3] must be zeroed first.
+int launch_mc_fused(const Code& c, uint64_t seed, uint64_t start, long long B, float p, const uint32_t pats[4],
+                    uint32_t* sX, uint32_t* sZ, uint8_t* rec, int rec_stride, int32_t* iters, uint32_t* merge,
+                    int32_t* listX, int32_t* listZ, int32_t* listS, uint32_t* counts, const uint64_t* imp_cols,
+                    unsigned long long* counters, bool survivors, hipStream_t st)
+{
+    FusedFn fused = nullptr, surv = nullptr;
+    if (!mc_fused_supported(c, rec_stride) || !fused_fns(c, fused, surv))
+        return fail(QEC_ERR_UNSUPPORTED, "mc fused: no kernel for this code or record layout");
+    if (B <= 0) return QEC_OK;
+    FusedArgs a{};
+    a.gp = make_gap(seed, p);
+    a.start = start; a.B = B; a.recB = rec_stride;
+    a.m = triage_masks(c, pats);
+    a.sX = sX; a.sZ = sZ; a.rec = rec; a.iters = iters; a.merge = merge;
+    a.listX = listX; a.listZ = listZ; a.listS = listS; a.counts = counts;
+    a.imp_cols = imp_cols; a.imp_cw = c.imp_col_words; a.counters = counters;
+    if (!survivors) {
+        const long long per = 64LL * kFusedWaves;
+        hipLaunchKernelGGL(fused, dim3((unsigned)((B + per - 1) / per)), dim3(64 * kFusedWaves), 0, st, a);
+    } else {
+        int dev = 0, cus = 256;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            cus <= 0)
+            cus = 256;
+        const long long per = 64LL * kSurvWaves;
+        const long long blocks = std::min<long long>((B + per - 1) / per, 2LL * cus);
+        hipLaunchKernelGGL(surv, dim3((unsigned)blocks), dim3(64 * kSurvWaves), 0, st, a);
+    }
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(QEC_ERR_HIP, std::string("mc fused launch: ") + hipGetErrorString(e));
+    return QEC_OK;
+}
+
+// the kernel loads rows with 16- / 8-byte loads (triage_sector)
+bool triage_aligned(const void* sX, const void* sZ)
+{
+    return ((reinterpret_cast<uintptr_t>(sX) | reinterpret_cast<uintptr_t>(sZ)) & 15u) == 0;
+}
+
 int launch_triage(const Code& c, const uint32_t* sX, const uint32_t* sZ, long long B, const uint32_t pats[4],
                   uint8_t* rec, int32_t* iters, uint32_t* merge, int32_t* listX, int32_t* listZ, uint32_t* counts,
                   hipStream_t st, int rec_stride)
@@ -391,11 +789,7 @@ int launch_triage(const Code& c, const uint32_t* sX, const uint32_t* sZ, long lo
     a.sX = sX; a.sZ = sZ; a.B = B;
     a.wX = (c.mX + 31) / 32; a.wZ = (c.mZ + 31) / 32;
     a.nb = (c.n + 7) / 8; a.recB = rec_stride > 0 ? rec_stride : 2 * a.nb + 1;
-    a.hdpatX = pats[0]; a.cvpatX = pats[1]; a.hdpatZ = pats[2]; a.cvpatZ = pats[3];
-    a.symX = by_count(pats[0], c.J, a.hdcntX) && by_count(pats[1], c.J, a.cvcntX);
-    a.symZ = by_count(pats[2], c.K, a.hdcntZ) && by_count(pats[3], c.K, a.cvcntZ);
-    const char* trees = std::getenv("QEC_TRIAGE_TREES");  // tests: force the pattern-tree form
-    if (trees && trees[0] == '1') a.symX = a.symZ = 0;
+    a.m = triage_masks(c, pats);
     a.rec = rec; a.iters = iters; a.merge = merge; a.listX = listX; a.listZ = listZ; a.counts = counts;
     const long long per_block = 64LL * kTriageWaves;
     const size_t smem = (size_t)kTriageWaves * (64 * a.recB + 16);

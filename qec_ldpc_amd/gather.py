@@ -11,23 +11,32 @@ import numpy as np
 
 def gather_records(packed, dst=0, group=None):
     """Gathers equally sized [B, R] uint8 record tensors of every rank to `dst`: returns the
-    [world * B, R] tensor (rank order = sample order) on dst, None elsewhere."""
+    [world * B, R] tensor (rank order = sample order) on dst, None elsewhere.  Without an
+    initialised process group (one process) it returns `packed` itself.
+
+    The collective follows from the backend alone, the same on every rank (no fallback that
+    could leave ranks in different collectives): gloo gathers host copies; nccl (RCCL over
+    xGMI) gathers the device tensors straight into the output's row blocks.  Only dst
+    allocates the output."""
     import torch
     import torch.distributed as dist
+    if not dist.is_initialized():
+        return packed
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
-    if world == 1:
-        return packed
-    if packed.is_cuda and dist.get_backend(group) == "gloo":  # gloo gathers host tensors
-        full = gather_records(packed.cpu(), dst, group)
-        return None if full is None else full.to(packed.device)
-    out = torch.empty((world * packed.shape[0], packed.shape[1]), dtype=packed.dtype, device=packed.device)
-    try:
-        parts = list(out.chunk(world)) if rank == dst else None
-        dist.gather(packed.contiguous(), gather_list=parts, dst=dst, group=group)
-    except (RuntimeError, ValueError, NotImplementedError):
-        dist.all_gather_into_tensor(out, packed.contiguous(), group=group)
-    return out if rank == dst else None
+    root = rank == dst
+    if dist.get_backend(group) == "gloo":
+        src = packed.detach().cpu().contiguous()
+        parts = [torch.empty_like(src) for _ in range(world)] if root else None
+        dist.gather(src, gather_list=parts, dst=dst, group=group)
+        if not root:
+            return None
+        full = torch.cat(parts)
+        return full.to(packed.device) if packed.is_cuda else full
+    out = torch.empty((world * packed.shape[0], packed.shape[1]), dtype=packed.dtype,
+                      device=packed.device) if root else None
+    dist.gather(packed.contiguous(), gather_list=list(out.chunk(world)) if root else None, dst=dst, group=group)
+    return out
 
 
 def unpack_records(records, n):

@@ -89,14 +89,45 @@ def test_statistics_kernel_matches_oracle(env, key, B, p, N):
 
 
 @pytest.mark.parametrize("stop", ["ref", "syndrome", "fixed"])
-@pytest.mark.parametrize("key,count,p", [("P7", 5000, 0.05), ("P61", 400, 0.04)])
+@pytest.mark.parametrize("key,count,p", [("P7", 5000, 0.05), ("P61", 400, 0.04), ("P7", 20000, 0.005),
+                                         ("P61", 3000, 0.01), ("P61", 3000, 0.002)])
 def test_monte_carlo_matches_oracle(env, key, count, p, stop):
+    """At p <= 0.01 the syndrome stop takes the fused low-p pipeline (triage.hip)."""
     code, dec, orc = env[key]
     r = dec.monte_carlo(0xBEEF, 17, count, p, 25, stop, batch=1000)
     x, z = depolarizing(0xBEEF, 17, count, code.n, p)
     exp, it = oracle_counters(orc, x, z, p, 25, stop)
     assert {k: r[k] for k in q.MC_COUNTERS} == exp
     assert r["tested"] == count
+    assert r["iterationsX"] == int(it[:, 0].sum()) and r["iterationsZ"] == int(it[:, 1].sum())
+
+
+@pytest.mark.parametrize("stop", ["ref", "syndrome", "fixed"])
+def test_monte_carlo_other_code_with_i_minus_p(tmp_path, stop):
+    """qec_monte_carlo on a code of neither shipped size (J=2,K=3,L=6,P=11, n = 66: records of 19 B,
+    packed errors of 18 B) with an I-P line: the Philox pipeline keeps the public 2 ceil(n/8) + 1 record
+    rows where the lane statistics kernel has no shape for padded ones, and its counters equal the
+    oracle's counting over the same file (any 0/1 matrix on line 4 is a valid CheckLogicalError input,
+    QEC_LDPC/Quantum_LDPC_Code.h:126-142)."""
+    g = q.QC_LDPC_CSS(2, 3, 6, 11, 2, 3)
+    rng = np.random.default_rng(11)
+    imp = (rng.random((2 * g.n, 2 * g.n)) < 0.02).astype(np.uint8)
+    path = str(tmp_path / "gen_imp.txt")
+    with open(path, "w") as f:
+        f.write("2 3 6 11 2 3\n")
+        f.write("\t".join(map(str, g.pcm(0).ravel())) + "\n")
+        f.write("\t".join(map(str, g.pcm(1).ravel())) + "\n")
+        f.write("\t".join(map(str, imp.ravel())) + "\n")
+    code = q.Quantum_LDPC_Code.createFromFile(path)
+    dec = q.DecoderGPU(code, 0)
+    assert "runtime-shift" in dec.describe()
+    orc = OracleCode(path)
+    count, p = 3000, 0.05
+    r = dec.monte_carlo(0xC0DE, 5, count, p, 25, stop, batch=1024)
+    x, z = depolarizing(0xC0DE, 5, count, code.n, p)
+    exp, it = oracle_counters(orc, x, z, p, 25, stop)
+    assert {k: r[k] for k in q.MC_COUNTERS} == exp
+    assert exp["logical"] > 0 and exp["corrected"] > 0  # both outcomes of the I-P check occur
     assert r["iterationsX"] == int(it[:, 0].sum()) and r["iterationsZ"] == int(it[:, 1].sum())
 
 

@@ -51,7 +51,7 @@ def test_packed_matches_oracle(env, key, stop, B):
 
 
 @pytest.mark.parametrize("key", ["P7", "P61"])
-@pytest.mark.parametrize("schedule,split", [(0, 0), (2, 0), (0, 2), (2, 2), (1, 1)])
+@pytest.mark.parametrize("schedule,split", [(0, 0), (2, 0), (0, 2), (2, 2), (1, 1), (0, 3), (2, 3)])
 def test_packed_dev_equals_byte_form(env, key, schedule, split):
     code, dec, _ = env[key]
     B = 5000

@@ -234,12 +234,13 @@ def test_cycle_jump_bit_identical(env, key, N):
 
 
 @pytest.mark.parametrize("key", ["P7", "P61"])
-@pytest.mark.parametrize("schedule,split", [(0, 0), (0, 2), (2, 0), (2, 2), (3, 0), (3, 2)])
+@pytest.mark.parametrize("schedule,split", [(0, 0), (0, 2), (2, 0), (2, 2), (3, 0), (3, 2), (0, 3), (2, 3)])
 @pytest.mark.parametrize("B", [1, 2, 383])
 def test_schedule_and_split_bit_identical(env, key, schedule, split, B):
     """QEC_OPT_SCHEDULE (waves take syndromes heaviest-first, schedule.hip) and
-    QEC_OPT_SECTOR_SPLIT (X and Z of a syndrome in two waves, flags merged by atomicOr)
-    change only which wave decodes what: every output bit equals the oracle's under every
+    QEC_OPT_SECTOR_SPLIT (X and Z of a syndrome in two waves, flags merged by atomicOr; 3: two
+    sector launches, the Z launch ORing its flags into the X launch's byte) change only which
+    wave decodes what: every output bit equals the oracle's under every
     stop rule, for a single syndrome, two, and a ragged batch (P7 packs 9 per wave)."""
     code, dec, _ = env[key]
     sX, sZ = mixed_inputs(code, max(B, 4), 91 + B, 0.02)
@@ -268,10 +269,12 @@ def test_split_flags_unaligned_and_dirty(env, key):
     tX, tZ = torch.from_numpy(sX).to(dev), torch.from_numpy(sZ).to(dev)
     eX = torch.empty((B, code.n), dtype=torch.uint8, device=dev)
     eZ = torch.empty((B, code.n), dtype=torch.uint8, device=dev)
-    for off, sched in ((0, 0), (1, 0), (2, 0), (3, 0), (1, 2), (2, 2), (3, 3)):  # schedule 2: the order pass zeroes flags
+    # schedule 2: the order pass zeroes flags; split 3: sector launches (X stores, Z ORs into that byte)
+    for off, sched, split in ((0, 0, 2), (1, 0, 2), (2, 0, 2), (3, 0, 2), (1, 2, 2), (2, 2, 2), (3, 3, 2),
+                              (1, 0, 3), (3, 2, 3)):
         buf = torch.full((B + 8,), 0xA5, dtype=torch.uint8, device=dev)
         fl = buf[off:off + B]
-        dec.set_option("sector_split", 2)
+        dec.set_option("sector_split", split)
         dec.set_option("schedule", sched)
         try:
             dec.decode_batch_dev(tX, tZ, 0.05, 20, "fixed", eX, eZ, fl)

@@ -118,19 +118,36 @@ def test_monte_carlo_triage_counters(env, key, p):
     code, dec, _ = env[key]
     B = 1 << 18
     res = {}
-    for tri in (2, 1, 0):
+    for tri in (2, 1, 3, 0):  # 2 / 1: the fused kernel (1 only up to p = 0.01), 3: triage kernel, 0: none
         dec.set_option("triage", tri)
         res[tri] = dec.monte_carlo(0x51EC0DE, 12345, B, p, 50, "syndrome")
     dec.set_option("triage", 1)
     for k in q.MC_COUNTERS + ("tested", "iterationsX", "iterationsZ"):
-        assert res[2][k] == res[1][k] == res[0][k], (k, res[2][k], res[1][k], res[0][k])
+        assert res[2][k] == res[1][k] == res[3][k] == res[0][k], (k, res[2][k], res[1][k], res[3][k], res[0][k])
+
+
+@pytest.mark.parametrize("key", ["P7", "P61"])
+@pytest.mark.parametrize("p,count,batch", [(0.001, 100003, 32768), (0.005, 70001, 65536), (0.01, 4097, 1000),
+                                           (0.0, 3000, 1024), (0.01, 1, 1)])
+def test_monte_carlo_fused_ragged(env, key, p, count, batch):
+    """The fused low-p pipeline (QEC_OPT_TRIAGE 1, triage.hip mc_fused_kernel + list decode + survivor
+    statistics) over ragged multi-batch runs, p = 0 (no errors at all) and a single sample: counters
+    equal the plain pipeline's (no triage) on the same samples."""
+    code, dec, _ = env[key]
+    res = {}
+    for tri in (1, 0):
+        dec.set_option("triage", tri)
+        res[tri] = dec.monte_carlo(0xFEED, 777, count, p, 50, "syndrome", batch)
+    dec.set_option("triage", 1)
+    for k in q.MC_COUNTERS + ("tested", "iterationsX", "iterationsZ"):
+        assert res[1][k] == res[0][k], (k, res[1][k], res[0][k])
 
 
 def test_triage_option_roundtrip(env):
     _, dec, _ = env["P61"]
     assert dec.get_option("triage") == 1
-    for v in (0, 2, 1):
+    for v in (0, 2, 3, 1):
         dec.set_option("triage", v)
         assert dec.get_option("triage") == v
     with pytest.raises(q.QecError):
-        dec.set_option("triage", 3)
+        dec.set_option("triage", 4)

@@ -15,6 +15,7 @@ workload.
 
 Usage: python tools/gpu/pmc_summary.py --dir gpurun_out/prof_TAG/p61 --code p61
        --bench gpurun_out/prof_TAG/p61/bench_trace.json --out profiles/pmc_p61.json
+(tools/gpu/run_profile.sh runs the passes and this summary per workload).
 """
 import argparse
 import csv
@@ -83,7 +84,9 @@ def main():
     durs = trace_duration_ns(os.path.join(a.dir, "trace"))
     dur_ns = sum(durs) / len(durs) if durs else None
     out = {"code": a.code, "batch": batch, "iters": b["config"]["bp_iters"], "stop": b["config"]["stop"],
-           "p": b["config"]["p"], "output": b["config"].get("output"), **meta,
+           "p": b["config"]["p"], "output": b["config"].get("output"), "hard_paths": b["config"].get("hard_paths", 1),
+           "input": b["config"].get("input", "bytes"),
+           **meta,
            "dispatches": {k: len(v) for k, v in vals.items()},
            "kernel_trace_avg_ns": dur_ns, "kernel_trace_dispatches": len(durs)}
     per_launch = {k: round(v) for k, v in avg.items()}

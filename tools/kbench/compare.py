@@ -2,6 +2,7 @@
 batch in one process, interleaved, and check that every variant's outputs are
 bit-identical to the first one's.  Usage:
   python tools/kbench/compare.py --code p61 --reps 5 v0 v1 ...
+  python tools/kbench/compare.py --mc --stop 2 --p 0.002 --batch 1048576 v0 v1 ...   (qec_monte_carlo runs)
 """
 import argparse
 import ctypes
@@ -36,7 +37,48 @@ def bind(path):
     L.qec_decoder_describe.argtypes = [vp, ctypes.c_char_p, ctypes.c_size_t]
     L.qec_last_error.restype = ctypes.c_char_p
     L.qec_decoder_set_option.argtypes = [vp, ctypes.c_int, ctypes.c_int]
+    from qec_ldpc_amd import MCResult
+    L.qec_monte_carlo.restype = ctypes.c_int
+    L.qec_monte_carlo.argtypes = [vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_float, ctypes.c_int,
+                                  ctypes.c_int, ctypes.c_size_t, ctypes.POINTER(MCResult)]
     return L
+
+
+def mc_main(a, name, p, iters):
+    """--mc: whole qec_monte_carlo runs (the psweep step) of every variant, interleaved; counters must
+    be identical; wall time of the call and its decode-kernel time."""
+    import time
+    from qec_ldpc_amd import MCResult
+    opts = {v: [kv.split("=") for kv in v.split(":", 1)[1].split(",")] if ":" in v else [] for v in a.variants}
+    runs = {}
+    for v in a.variants:
+        L = bind(os.path.join(ROOT, "build", "variants", v.split(":")[0], "libqecldpc.so"))
+        c = L.qec_code_load(code_path(name).encode())
+        d = L.qec_decoder_create(c, 0, 0)
+        for k, val in opts[v]:
+            assert L.qec_decoder_set_option(d, OPTIONS[k], int(val)) == 0, L.qec_last_error()
+        runs[v] = (L, d)
+    res = {v: [] for v in a.variants}
+    cnt = {}
+    for rep in range(a.reps + 1):
+        for v, (L, d) in runs.items():
+            r = MCResult()
+            t = time.perf_counter()
+            rc = L.qec_monte_carlo(d, 0x51EC0DE, 0, a.batch, p, iters, a.stop, a.batch, ctypes.byref(r))
+            dt = time.perf_counter() - t
+            assert rc == 0, L.qec_last_error()
+            c = r.as_dict()
+            key = tuple(c[k] for k in ("tested", "withX", "withZ", "synX", "synZ", "logical", "corrected", "convX",
+                                       "convZ", "iterationsX", "iterationsZ"))
+            cnt.setdefault(v, key)
+            assert cnt[v] == key
+            if rep:
+                res[v].append((dt, c["decodeSeconds"]))
+    ref = cnt[a.variants[0]]
+    for v in a.variants:
+        ms = float(np.median([x[0] for x in res[v]])) * 1e3
+        dms = float(np.median([x[1] for x in res[v]])) * 1e3
+        print("%-22s %9.3f ms  %12.0f syn/s  decode %.3f ms  identical=%s" % (v, ms, a.batch / ms * 1e3, dms, cnt[v] == ref))
 
 
 def main():
@@ -47,6 +89,7 @@ def main():
     ap.add_argument("--stop", type=int, default=1)
     ap.add_argument("--iters", type=int, default=None)
     ap.add_argument("--p", type=float, default=None, help="depolarising rate (default: the code's bench p)")
+    ap.add_argument("--mc", action="store_true", help="whole Monte-Carlo runs (qec_monte_carlo, --batch samples)")
     ap.add_argument("variants", nargs="+")
     a = ap.parse_args()
     name, p, iters = CODES[a.code]
@@ -54,6 +97,8 @@ def main():
         iters = a.iters
     if a.p is not None:
         p = a.p
+    if a.mc:
+        return mc_main(a, name, p, iters)
     dev = torch.device("cuda", 0)
     # a variant is "<build dir>" or "<build dir>:<option>=<value>,..." (decoder options, e.g.
     # cur:cycle_jump=0), so one build can be timed with several option settings

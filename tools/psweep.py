@@ -39,6 +39,21 @@ def summarize(p, c, seconds, world):
     }
 
 
+def reduce_counters(r, times, backend, dev):
+    """Sums the per-rank counters and takes the max of the per-rank times across ranks (one
+    all-reduce each, on the device for RCCL, on the host for gloo); without an initialised
+    process group (one process) returns them as they are."""
+    import torch
+    import torch.distributed as dist
+    cdev = dev if backend in (None, "nccl") else torch.device("cpu")  # gloo reduces host tensors
+    vec = torch.tensor([r[k] for k in FIELDS], dtype=torch.int64, device=cdev)
+    tm = torch.tensor(times, dtype=torch.float64, device=cdev)
+    if dist.is_initialized():
+        dist.all_reduce(vec)
+        dist.all_reduce(tm, op=dist.ReduceOp.MAX)
+    return dict(zip(FIELDS, vec.cpu().tolist())), [float(x) for x in tm.cpu().tolist()]
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--code", default="J_4_K_5_L_10_P_61_s_9_t_49")
@@ -97,18 +112,12 @@ def main():
         same = all(all(r[k] == runs[0][1][k] for k in FIELDS) for _, r in runs)
         order = sorted(range(len(runs)), key=lambda i: runs[i][0])
         dt, r = runs[order[len(order) // 2]]
-        cdev = dev if backend in (None, "nccl") else torch.device("cpu")  # gloo reduces host tensors
-        vec = torch.tensor([r[k] for k in FIELDS], dtype=torch.int64, device=cdev)
-        tm = torch.tensor([dt, r["decodeSeconds"], runs[order[0]][0], runs[order[-1]][0], 0.0 if same else 1.0],
-                          dtype=torch.float64, device=cdev)
-        if world > 1:
-            dist.all_reduce(vec)
-            dist.all_reduce(tm, op=dist.ReduceOp.MAX)
-        c = dict(zip(FIELDS, vec.cpu().tolist()))
-        line = summarize(p, c, float(tm[0].item()), world)
-        line["decode_seconds"] = round(float(tm[1].item()), 4)  # decode kernels only (the rest: front end + counts)
-        line["reps"] = {"n": len(runs), "reported": "median", "min_seconds": round(float(tm[2].item()), 4),
-                        "max_seconds": round(float(tm[3].item()), 4), "counters_identical": float(tm[4].item()) == 0.0}
+        c, tm = reduce_counters(r, [dt, r["decodeSeconds"], runs[order[0]][0], runs[order[-1]][0], 0.0 if same else 1.0],
+                                backend, dev)
+        line = summarize(p, c, tm[0], world)
+        line["decode_seconds"] = round(tm[1], 4)  # decode kernels only (the rest: front end + counts)
+        line["reps"] = {"n": len(runs), "reported": "median", "min_seconds": round(tm[2], 4),
+                        "max_seconds": round(tm[3], 4), "counters_identical": tm[4] == 0.0}
         if backend:
             line["backend"] = backend
         line.update({"code": code.describe(), "stop": args.stop, "max_iters": args.iters, "seed": args.seed})

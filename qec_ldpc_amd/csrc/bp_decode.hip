@@ -280,6 +280,7 @@ struct BpArgs {
     const int32_t* listX;
     const int32_t* listZ;
     const uint32_t* counts;
+    int mergeOnly;  // list mode for the fused Monte-Carlo pipeline: flags only into merge[] (no record byte)
     long long B;
     int P, G, n, mX, mZ;
     int nb, recBytes;  // ceil(n / 8); row stride of the records (2 nb + 1, or padded to whole words)
@@ -1473,9 +1474,11 @@ constexpr int waves_per_block() { return QEC_WAVES_PER_BLOCK > 0 ? QEC_WAVES_PER
 // (stores its flags), 4: sector Z of a sector launch, enqueued after the X launch on the same stream
 // (ORs its flags into the byte the X launch stored).  Modes 3 and 4 compile one sector only, so each
 // kernel's registers are allocated for that sector alone.
+// pre: the sector's syndrome bits were loaded by the caller (sbPre; list mode, one sector per wave)
 template <int RX, int RZ, int L, int STOP, class SH, class TU, int MODE>
 __device__ __forceinline__ void decode_group(const BpArgs& a, const float* __restrict__ tab0, uint8_t* __restrict__ stage,
-                                             int i, int gb, uint32_t b, bool in_range, bool doX)
+                                             int i, int gb, uint32_t b, bool in_range, bool doX, bool pre = false,
+                                             uint32_t sbPre = 0u)
 {
     constexpr bool SPLIT = MODE != 0;
     constexpr bool kHasX = MODE != 4, kHasZ = MODE != 3;
@@ -1491,13 +1494,13 @@ __device__ __forceinline__ void decode_group(const BpArgs& a, const float* __res
 #endif
     const bool runX = kHasX && doX, runZ = kHasZ && (!doX || !SPLIT);
     // both sectors' syndrome loads are issued up front: the Z load's latency hides behind X
-    const uint32_t sbX = runX ? load_sbits<RX, 0, SH>(a, ln, b, in_range) : 0u;
-    uint32_t sbZ = (QEC_PREFETCH_Z && runZ) ? load_sbits<RZ, 1, SH>(a, ln, b, in_range) : 0u;
+    const uint32_t sbX = pre ? sbPre : runX ? load_sbits<RX, 0, SH>(a, ln, b, in_range) : 0u;
+    uint32_t sbZ = pre ? sbPre : (QEC_PREFETCH_Z && runZ) ? load_sbits<RZ, 1, SH>(a, ln, b, in_range) : 0u;
     if constexpr (kHasX) {
         if (runX) decode_sector<RX, L, 0, STOP, SH, TU>(a, ln, b, in_range, pp, sbX, tab0, flags, itX, stage);
     }
     if constexpr (kHasZ) {
-        if (!QEC_PREFETCH_Z && runZ) sbZ = load_sbits<RZ, 1, SH>(a, ln, b, in_range);
+        if (!pre && !QEC_PREFETCH_Z && runZ) sbZ = load_sbits<RZ, 1, SH>(a, ln, b, in_range);
         if (runZ) decode_sector<RZ, L, 1, STOP, SH, TU>(a, ln, b, in_range, pp, sbZ, tab0 + kTabX, flags, itZ, stage);
     }
     if (in_range && lane_i<SH>(ln) == 0) {
@@ -1506,6 +1509,10 @@ __device__ __forceinline__ void decode_group(const BpArgs& a, const float* __res
             *fdst = (uint8_t)flags;
         } else if constexpr (MODE == 4) {
             *fdst = (uint8_t)(*fdst | flags);  // the X launch's byte (same stream, earlier launch)
+        } else if (MODE == 2 && a.mergeOnly) {
+            // the fused Monte-Carlo pipeline reads the flags from the merge word itself
+            // (mc_survivor_kernel): no returned value to wait for
+            __hip_atomic_fetch_or(&a.merge[b], flags, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         } else {
             // the two sectors meet in the syndrome's merge word: whichever finds the other's done
             // bit already set writes the merged byte
@@ -1568,12 +1575,30 @@ void bp_decode_kernel(const BpArgs a)
         const long long nX = a.counts[0], nZ = a.counts[1];
         const long long wXn = (nX + G - 1) / G, wTot = wXn + (nZ + G - 1) / G;
         const long long nw = (long long)gridDim.x * (blockDim.x >> 6);
-        for (long long vw = wave; vw < wTot; vw += nw) {
-            const bool doX = vw < wXn;  // wave-uniform
-            const long long slot = (doX ? vw : vw - wXn) * G + g;
-            const bool in_range = (g < G) && (slot < (doX ? nX : nZ));
-            const uint32_t b = in_range ? (uint32_t)(doX ? a.listX : a.listZ)[slot] : 0u;
-            decode_group<RX, RZ, L, STOP, SH, TU, 2>(a, tab0, stage, i, gb, b, in_range, doX);
+        // software pipelined: the list entry two sectors ahead and the syndrome bits of the next one
+        // are in flight while a sector decodes (each is otherwise a dependent global load at its start)
+        Lane lq{i, gb, 0, 0, false};
+        auto entry = [&](long long vw, bool& dX, bool& ir) -> uint32_t {
+            dX = vw < wXn;  // wave-uniform
+            const long long slot = (dX ? vw : vw - wXn) * G + g;
+            ir = vw < wTot && (g < G) && (slot < (dX ? nX : nZ));
+            return ir ? (uint32_t)(dX ? a.listX : a.listZ)[slot] : 0u;
+        };
+        auto bits = [&](uint32_t b, bool dX, bool ir) -> uint32_t {
+            return dX ? load_sbits<RX, 0, SH>(a, lq, b, ir) : load_sbits<RZ, 1, SH>(a, lq, b, ir);
+        };
+        long long vw = wave;
+        bool dX0, ir0, dX1, ir1;
+        uint32_t b0 = entry(vw, dX0, ir0);
+        uint32_t b1 = entry(vw + nw, dX1, ir1);
+        uint32_t sb0 = bits(b0, dX0, ir0);
+        for (; vw < wTot; vw += nw) {
+            bool dX2, ir2;
+            const uint32_t b2 = entry(vw + 2 * nw, dX2, ir2);
+            const uint32_t sb1 = vw + nw < wTot ? bits(b1, dX1, ir1) : 0u;
+            decode_group<RX, RZ, L, STOP, SH, TU, 2>(a, tab0, stage, i, gb, b0, ir0, dX0, true, sb0);
+            b0 = b1; dX0 = dX1; ir0 = ir1; sb0 = sb1;
+            b1 = b2; dX1 = dX2; ir1 = ir2;
         }
         return;
     }
@@ -1610,7 +1635,10 @@ struct TuneP61MinReg : TuneP61 {};
 using ShiftsP61 = GeneratedShifts<4, 5, 10, 61, 9, 49, TuneP61::kRelabel, TuneP61::kMaskSelect>;
 // P7: three columns per division guard (col_group): 0.075 vs 0.077 ms at configs[1] (65 536 @ 20), even
 // at 2^20 (profiles/r03/cmp_p7_65536_colgroups.txt, cmp_p7_2e20.txt)
-using TuneP7 = Tune<8, true, false, true, true, true, false, 2, 1, 7, 3>;
+#ifndef QEC_P7_MINW
+#define QEC_P7_MINW 8
+#endif
+using TuneP7 = Tune<QEC_P7_MINW, true, false, true, true, true, false, 2, 1, 7, 3>;
 struct TuneP7MinReg : TuneP7 {};
 using ShiftsP7 = GeneratedShifts<3, 3, 6, 7, 2, 3, TuneP7::kRelabel, TuneP7::kMaskSelect>;
 #ifndef QEC_P61_MINREG
@@ -1982,7 +2010,7 @@ bool decode_pattern_masks(const void* variant, float errorProbability, uint32_t 
 int launch_decode_list(const void* variant, const Code& c, const uint8_t* sX, const uint8_t* sZ, long long B,
                        float errorProbability, int maxIter, int hardPaths, uint8_t* rec, int32_t* iters,
                        uint32_t* merge, const int32_t* listX, const int32_t* listZ, const uint32_t* counts,
-                       hipStream_t stream, int rec_stride)
+                       hipStream_t stream, int rec_stride, bool merge_only)
 {
     const Variant* v = static_cast<const Variant*>(variant);
     if (!v->list) return fail(QEC_ERR_UNSUPPORTED, "bp_decode: no list-mode kernel for this code");
@@ -1992,7 +2020,7 @@ int launch_decode_list(const void* variant, const Code& c, const uint8_t* sX, co
     a.sX = sX; a.sZ = sZ; a.sbits = 1;
     a.wX = (c.mX + 31) / 32; a.wZ = (c.mZ + 31) / 32;
     a.rec = rec; a.iters = iters; a.merge = merge;
-    a.listX = listX; a.listZ = listZ; a.counts = counts;
+    a.listX = listX; a.listZ = listZ; a.counts = counts; a.mergeOnly = merge_only ? 1 : 0;
     a.B = B; a.P = c.P; a.G = 64 / c.P;
     a.n = c.n; a.mX = c.mX; a.mZ = c.mZ;
     a.nb = (c.n + 7) / 8; a.recBytes = rec_stride > 0 ? rec_stride : 2 * a.nb + 1;

@@ -23,14 +23,14 @@ size_t schedule_workspace_bytes(long long B, int mX, int mZ);
 long long schedule_max_batch();
 long long schedule_local_max_batch();
 int launch_schedule(const uint8_t* sX, const uint8_t* sZ, bool sbits, long long B, int mX, int mZ, void* ws,
-                    uint32_t* zero_merge, int32_t** perm_out, hipStream_t st, int method);
+                    uint32_t* zero_merge, int32_t** perm_out, hipStream_t st, int method, uint32_t* bar);
 bool decode_uses_split(const void* variant, int stop, int split, long long B);
 bool decode_has_list(const void* variant);
 bool decode_pattern_masks(const void* variant, float errorProbability, uint32_t pats[4]);
 int launch_decode_list(const void* variant, const Code& c, const uint8_t* sX, const uint8_t* sZ, long long B,
                        float errorProbability, int maxIter, int hardPaths, uint8_t* rec, int32_t* iters,
                        uint32_t* merge, const int32_t* listX, const int32_t* listZ, const uint32_t* counts,
-                       hipStream_t stream, int rec_stride = 0);
+                       hipStream_t stream, int rec_stride, bool merge_only);
 bool triage_supported(const Code& c);
 bool triage_aligned(const void* sX, const void* sZ);
 int launch_triage(const Code& c, const uint32_t* sX, const uint32_t* sZ, long long B, const uint32_t pats[4],
@@ -77,6 +77,22 @@ struct qec_code {
 
 // One decoder handle: a device engine (wave-circulant variant or sparse-graph plan) plus the
 // workspaces its entry points share, or a multi-device group of such handles (parts).
+// Events owned by a handle (created on first use, destroyed with it on its device).
+struct EventSet {
+    std::vector<hipEvent_t> ev;
+    ~EventSet()
+    {
+        for (hipEvent_t e : ev) (void)hipEventDestroy(e);
+    }
+    int make(size_t n, unsigned flags)
+    {
+        ev.assign(n, nullptr);
+        for (auto& e : ev)
+            if (hipEventCreateWithFlags(&e, flags) != hipSuccess) return qec::fail(QEC_ERR_HIP, "hipEventCreateWithFlags");
+        return QEC_OK;
+    }
+};
+
 struct qec_decoder {
     std::shared_ptr<const Code> code;
     int device = 0;
@@ -96,6 +112,7 @@ struct qec_decoder {
     // on another stream waits for it (stream-ordered reuse)
     DeviceArray<uint8_t> sched;
     DeviceArray<uint32_t> merge;
+    DeviceArray<uint32_t> gbar;  // grid-barrier words of the one-launch dispatch order (zeroed at creation)
     DeviceArray<int32_t> tlist;  // triage: listX [B], listZ [B], (fused Monte-Carlo: listS [B]), counts
     hipEvent_t ws_ev = nullptr;
     hipStream_t ws_stream = nullptr;
@@ -110,6 +127,7 @@ struct qec_decoder {
     DeviceArray<uint8_t> msX, msZ, merrp, mrec, mtype;
     DeviceArray<int32_t> mit, midx;
     DeviceArray<unsigned long long> mcount;
+    EventSet mc_ev;  // qec_monte_carlo's ring of decode-time event pairs
     // multi-device group (qec_decoder_create_multi): the parts do the work, this handle only routes
     std::vector<qec_decoder*> parts;
 
@@ -369,6 +387,10 @@ qec_decoder* qec_decoder_create_engine(const qec_code* h, int device, size_t max
                                 hipMemcpyHostToDevice), "I-P upload");
         }
         d->mcount.reserve(QEC_MC_NCOUNTERS_ALL);
+        if (d->variant) {
+            d->gbar.reserve(2);
+            hip_throw(hipMemset(d->gbar.data(), 0, 2 * sizeof(uint32_t)), "grid-barrier words");
+        }
     } catch (const std::exception& ex) {
         fail(QEC_ERR_HIP, std::string("qec_decoder_create: ") + ex.what());
         return nullptr;
@@ -570,7 +592,7 @@ int dispatch_decode(qec_decoder* d, const uint8_t* sX, const uint8_t* sZ, long l
                            iters, d->merge.data(), lX, lZ, cnt, st, rec_stride);
         if (!rc)
             rc = launch_decode_list(d->variant, c, sX, sZ, B, p, maxIter, hp, rec, iters, d->merge.data(), lX, lZ, cnt, st,
-                                    rec_stride);
+                                    rec_stride, false);
         if (rc) return rc;
         return ws_release(d, st);
     }
@@ -588,7 +610,7 @@ int dispatch_decode(qec_decoder* d, const uint8_t* sX, const uint8_t* sZ, long l
         // a sector-split launch merges its flags in zeroed words: the order pass zeroes them
         const int method = d->schedule == 3 ? QEC_ORDER_LOCAL : QEC_ORDER_GLOBAL;
         rc = launch_schedule(sX, sZ, sbits, B, c.mX, c.mZ, d->sched.data(), split ? d->merge.data() : nullptr, &pm, st,
-                             method);
+                             method, d->gbar.data());
         if (rc) return rc;
         perm = pm;
         zeroed = split;
@@ -833,7 +855,7 @@ int mc_batch(qec_decoder* d, McArgsHost h, int src, float p, int maxIter, int st
         for (int pass = 0; pass < 2; ++pass) {
             if (pass == 1) {
                 rc = launch_decode_list(d->variant, c, d->msX.data(), d->msZ.data(), B, p, maxIter, hard_path_bits(d),
-                                        d->mrec.data(), d->mit.data(), d->merge.data(), lX, lZ, cnt, st, rstride);
+                                        d->mrec.data(), d->mit.data(), d->merge.data(), lX, lZ, cnt, st, rstride, true);
                 if (rc) return rc;
                 if (ev1) QEC_HIP_CHECK(hipEventRecord(ev1, st));
             }
@@ -874,19 +896,6 @@ int mc_fetch_counters(qec_decoder* d, unsigned long long* out)
     return QEC_OK;
 }
 
-struct EventSet {
-    std::vector<hipEvent_t> ev;
-    ~EventSet()
-    {
-        for (hipEvent_t e : ev) (void)hipEventDestroy(e);
-    }
-    int make(size_t n, unsigned flags)
-    {
-        ev.assign(n, nullptr);
-        for (auto& e : ev) QEC_HIP_CHECK(hipEventCreateWithFlags(&e, flags));
-        return QEC_OK;
-    }
-};
 
 // qec_monte_carlo on one part: samples [start, start + count), counters left in d->mcount
 int monte_carlo_part(qec_decoder* d, uint64_t seed, uint64_t start, uint64_t count, float p, int maxIter, int stop,
@@ -900,8 +909,8 @@ int monte_carlo_part(qec_decoder* d, uint64_t seed, uint64_t start, uint64_t cou
     // decode-kernel time from a ring of event pairs: the host waits only on a pair it reuses,
     // kRing batches behind the launches (no per-batch synchronisation)
     constexpr size_t kRing = 32;
-    EventSet ev;
-    if ((rc = ev.make(2 * kRing, hipEventDefault))) return rc;
+    if (d->mc_ev.ev.empty() && (rc = d->mc_ev.make(2 * kRing, hipEventDefault))) return rc;  // once per handle
+    EventSet& ev = d->mc_ev;
     double dec = 0;
     uint64_t k = 0;
     auto harvest = [&](size_t slot) -> int {
@@ -1115,15 +1124,20 @@ int qec_monte_carlo(qec_decoder* d, uint64_t seed, uint64_t start, uint64_t coun
     std::vector<int> rcs(np, QEC_OK);
     std::vector<std::string> errs(np);
     std::vector<double> dec(np, 0.0);
-    std::vector<std::thread> th;
-    for (int j = 0; j < np; ++j) {
-        const uint64_t lo = (uint64_t)shard_lo((long long)count, j, np), hi = (uint64_t)shard_lo((long long)count, j + 1, np);
-        th.emplace_back([&, j, lo, hi] {
-            rcs[j] = monte_carlo_part(parts[j], seed, start + lo, hi - lo, p, maxIter, stop, batch, &dec[j]);
-            if (rcs[j]) errs[j] = last_error_cstr();
-        });
+    if (np == 1) {  // one device: no host thread
+        rcs[0] = monte_carlo_part(parts[0], seed, start, count, p, maxIter, stop, batch, &dec[0]);
+        if (rcs[0]) errs[0] = last_error_cstr();
+    } else {
+        std::vector<std::thread> th;
+        for (int j = 0; j < np; ++j) {
+            const uint64_t lo = (uint64_t)shard_lo((long long)count, j, np), hi = (uint64_t)shard_lo((long long)count, j + 1, np);
+            th.emplace_back([&, j, lo, hi] {
+                rcs[j] = monte_carlo_part(parts[j], seed, start + lo, hi - lo, p, maxIter, stop, batch, &dec[j]);
+                if (rcs[j]) errs[j] = last_error_cstr();
+            });
+        }
+        for (auto& t : th) t.join();
     }
-    for (auto& t : th) t.join();
     unsigned long long cn[QEC_MC_NCOUNTERS_ALL] = {};
     for (int j = 0; j < np; ++j) {
         if (rcs[j]) return fail(rcs[j], "part " + std::to_string(j) + ": " + errs[j]);

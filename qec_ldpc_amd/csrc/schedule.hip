@@ -282,6 +282,60 @@ __global__ __launch_bounds__(kScatThreads) void schedule_scatter_fused_kernel(co
 // (A cooperative single launch -- histogram, grid barrier, scatter -- was measured 4x slower than the
 // two launches at P7 65 536: 0.288 vs 0.069 ms per decode call, hipLaunchCooperativeKernel's own cost;
 // profiles/r03/cmp_coop_order_p7_65536.txt.)
+//
+// The same single launch with an ordinary launch and a software grid barrier, for at most
+// kOneLaunchChunks workgroups of kScatThreads threads: that many fit the chip at once (one per CU at
+// most, a quarter of its wave slots; the decoder's stream runs nothing beside them), so every
+// workgroup of the grid is resident and the barrier cannot wait on one that was never scheduled.
+// bar[0] counts arrivals; bar[1] departures, and the last workgroup to leave zeroes both for the next
+// launch (bar comes zeroed from qec_decoder_create; graph replays reuse it the same way).
+constexpr int kOneLaunchChunks = 128;
+#ifndef QEC_SCHED_ONE_LAUNCH
+#define QEC_SCHED_ONE_LAUNCH 1
+#endif
+
+__device__ __forceinline__ void grid_arrive_wait(uint32_t* bar, uint32_t nblocks)
+{
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence();  // this workgroup's counts before its arrival
+        atomicAdd(&bar[0], 1u);
+        while (__hip_atomic_load(&bar[0], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < nblocks)
+            __builtin_amdgcn_s_sleep(2);
+        __threadfence();
+    }
+    __syncthreads();
+}
+
+__device__ __forceinline__ void grid_depart(uint32_t* bar, uint32_t nblocks)
+{
+    if (threadIdx.x == 0 && atomicAdd(&bar[1], 1u) == nblocks - 1) {
+        // every workgroup has passed the barrier: reset for the next launch (vector stores)
+        __hip_atomic_store(&bar[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&bar[1], 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+template <int MODE>  // 0: byte rows, 1: byte rows of at most kShortRows, 2: bit rows
+__global__ __launch_bounds__(kScatThreads) void schedule_one_launch_kernel(const uint8_t* __restrict__ sX,
+                                                                         const uint8_t* __restrict__ sZ, long long B,
+                                                                         int mX, int mZ, int chunk, int nch, int nbk,
+                                                                         uint8_t* __restrict__ key,
+                                                                         uint32_t* __restrict__ counts,
+                                                                         uint32_t* __restrict__ zero_merge,
+                                                                         int32_t* __restrict__ perm, uint32_t* bar)
+{
+    __shared__ uint32_t h[kBuckets];
+    __shared__ FusedLds s;
+    if constexpr (MODE == 2)
+        hist_bits_body(reinterpret_cast<const uint32_t*>(sX), reinterpret_cast<const uint32_t*>(sZ), B, mX, mZ, chunk, nbk,
+                       key, counts, zero_merge, h);
+    else
+        hist_body<MODE == 1 ? 1 : kHistSplitLong>(sX, sZ, B, mX, mZ, chunk, nbk, key, counts, zero_merge, h);
+    grid_arrive_wait(bar, (uint32_t)nch);
+    scatter_fused_body(key, B, chunk, nch, nbk, counts, perm, s);
+    grid_depart(bar, (uint32_t)nch);
+}
 
 // The whole order pass in one launch, for small batches (where the passes above are mostly launch
 // latency): workgroup c sorts its own chunk heaviest-first in LDS and interleaves the chunks by
@@ -377,9 +431,10 @@ size_t schedule_workspace_bytes(long long B, int, int)
 
 // Fills the workspace (schedule_workspace_bytes bytes) and returns in *perm_out the
 // heaviest-first order of the batch.  zero_merge (nullable): B words the hist pass zeroes on
-// the way (the sector-split decode merges its two sectors' flags there, bp_decode.hip).
+// the way (the sector-split decode merges its two sectors' flags there, bp_decode.hip).  bar
+// (nullable): the handle's two zeroed grid-barrier words (schedule_one_launch_kernel).
 int launch_schedule(const uint8_t* sX, const uint8_t* sZ, bool sbits, long long B, int mX, int mZ, void* ws,
-                    uint32_t* zero_merge, int32_t** perm_out, hipStream_t st, int method)
+                    uint32_t* zero_merge, int32_t** perm_out, hipStream_t st, int method, uint32_t* bar)
 {
     if (B > schedule_max_batch()) return fail(QEC_ERR_ARG, "schedule: batch too large to order");
     const bool shortrows = sbits || mX + mZ <= kShortRows;
@@ -423,6 +478,21 @@ int launch_schedule(const uint8_t* sX, const uint8_t* sZ, bool sbits, long long 
     // buckets: weights 0 .. mX + mZ (fused pass), 256 for the separate offsets / scatter passes
     int nbk = kBuckets;
     if (fused && mX + mZ + 1 < kBuckets) nbk = mX + mZ + 1 < 32 ? 32 : mX + mZ + 1;
+    if (QEC_SCHED_ONE_LAUNCH && fused && bar != nullptr && nch <= kOneLaunchChunks) {
+        // histogram, grid barrier, offsets and scatter in one launch (schedule_one_launch_kernel)
+        if (sbits)
+            hipLaunchKernelGGL(schedule_one_launch_kernel<2>, dim3(nch), dim3(kScatThreads), 0, st, sX, sZ, B,
+                               (mX + 31) / 32, (mZ + 31) / 32, chunk, nch, nbk, key, counts, zero_merge, perm, bar);
+        else if (shortrows)
+            hipLaunchKernelGGL(schedule_one_launch_kernel<1>, dim3(nch), dim3(kScatThreads), 0, st, sX, sZ, B, mX, mZ,
+                               chunk, nch, nbk, key, counts, zero_merge, perm, bar);
+        else
+            hipLaunchKernelGGL(schedule_one_launch_kernel<0>, dim3(nch), dim3(kScatThreads), 0, st, sX, sZ, B, mX, mZ,
+                               chunk, nch, nbk, key, counts, zero_merge, perm, bar);
+        const hipError_t err = hipGetLastError();
+        if (err != hipSuccess) return fail(QEC_ERR_HIP, std::string("schedule launch: ") + hipGetErrorString(err));
+        return QEC_OK;
+    }
     if (sbits)
         hipLaunchKernelGGL(schedule_hist_bits_kernel, dim3(nch), dim3(hthreads), 0, st,
                            reinterpret_cast<const uint32_t*>(sX), reinterpret_cast<const uint32_t*>(sZ), B, (mX + 31) / 32,

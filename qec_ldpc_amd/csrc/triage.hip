@@ -583,9 +583,10 @@ __global__ __launch_bounds__(64 * kFusedWaves) void mc_fused_kernel(const FusedA
 
 // The survivors' counters after the list-mode decode: lane per listed sample (grid-stride over
 // listS [0, counts[2])); the sample's errors are walked again into the lane's LDS region in the record
-// layout, XORed with its record (the final decisions), and counted as statistics_lane_kernel counts
-// a sample (syndrome fails from the flags byte, the I-P check when neither failed and the residual is
-// nonzero, convergence fails, both iteration counts).  withX / withZ were counted by mc_fused_kernel.
+// layout, XORed with its record's decisions, and counted as statistics_lane_kernel counts a sample
+// (syndrome fails from the flags -- the merge word's low byte --, the I-P check when neither failed and
+// the residual is nonzero, convergence fails, both iteration counts).  withX / withZ were counted by
+// mc_fused_kernel.
 constexpr int kSurvWaves = 4;
 
 template <int L, int P>
@@ -619,20 +620,21 @@ __global__ __launch_bounds__(64 * kSurvWaves) void mc_survivor_kernel(const Fuse
         }
         // residual = errors ^ decisions over the record's 2 nb decision bytes
         const uint32_t* __restrict__ r = reinterpret_cast<const uint32_t*>(a.rec + b * a.recB);
-        constexpr int kRW = (2 * nb + 1 + 3) / 4;  // record words holding decisions and the flags byte
+        constexpr int kRW = (2 * nb + 3) / 4;  // record words holding decisions
         static_assert(kRW <= 2 * NW, "the lane region holds the record's words");
-        uint32_t nz = 0, f = 0;
+        uint32_t nz = 0;
 #pragma unroll
         for (int k = 0; k < kRW; ++k) {
             const uint32_t rv = valid ? r[k] : 0u;
             const int rem = 2 * nb - 4 * k;  // decision bytes in word k
             const uint32_t m = rem >= 4 ? ~0u : rem <= 0 ? 0u : (1u << (8 * rem)) - 1u;
-            if (k == (2 * nb) / 4) f = (rv >> (8 * ((2 * nb) % 4))) & 0xFFu;
             const uint32_t res = (mine[k] ^ rv) & m;
             mine[k] = res;
             nz |= res;
         }
-        f = valid ? f : 0u;
+        // the flags: the list-mode decode ORs its sectors' into the merge word, which the fused kernel
+        // set to the stopped sectors' (launch_decode_list, merge_only); the record's byte is not merged
+        const uint32_t f = valid ? (a.merge[b] & 0xFFu) : 0u;
         const bool sx = (f & QEC_SYNDROME_FAIL_X) != 0, sz = (f & QEC_SYNDROME_FAIL_Z) != 0;
         unsigned long long need = __ballot(valid && !(sx || sz) && nz != 0u), logical = 0;
         while (need) {

@@ -11,6 +11,7 @@
 #   profile NAME [CODES] tools/gpu/run_profile.sh NAME CODES (PMC evidence; EXTRA="..." via env STEP_EXTRA)
 #   trace NAME [ARGS]    rocprofv3 --kernel-trace --stats of bench.py ARGS
 #   mctrace NAME [ARGS]  rocprofv3 --kernel-trace --stats of tools/psweep.py ARGS
+#   exec CMD             any other command (built beforehand on the CPU side)
 set -o pipefail
 R="$GRAFT_REPO_ROOT"
 TAG=$1; shift
@@ -48,6 +49,8 @@ for spec in "$@"; do
       (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/$name" -o run -- \
           python3 $prog $rest > "$O/${name}.out" 2> "$O/${name}.err"); rc=$?
       [ $rc -eq 0 ] && cut -d, -f1-4 "$O/$name/run_kernel_stats.csv" | cut -c1-140 | head -12;;
+    exec)
+      eval timeout -k 10 600 "$args" > "$O/exec_$i.txt" 2>&1; rc=$?; tail -5 "$O/exec_$i.txt" | cut -c1-300;;
     *) echo "unknown step $step"; rc=2;;
   esac
   echo "== step $i rc=$rc"

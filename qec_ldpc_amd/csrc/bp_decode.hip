@@ -281,6 +281,7 @@ struct BpArgs {
     const int32_t* listZ;
     const uint32_t* counts;
     int mergeOnly;  // list mode for the fused Monte-Carlo pipeline: flags only into merge[] (no record byte)
+    int countStride;  // list mode: counts[0] = listX length, counts[countStride] = listZ length
     long long B;
     int P, G, n, mX, mZ;
     int nb, recBytes;  // ceil(n / 8); row stride of the records (2 nb + 1, or padded to whole words)
@@ -501,8 +502,18 @@ __device__ __forceinline__ bool band(bool a, bool b) { return (int)a & (int)b; }
 //   (profiles/r01/session5/div_check.json).
 // The guard below is evaluated for a whole column of divisions and the short path taken only
 // when every live lane of the wave passes it; otherwise the full sequence runs.
+//   QEC_DIV4  experiment: the short form without the reciprocal refinement (4 instructions; valid only if
+//             tools/kbench/div4_check.hip finds it equal to the IEEE quotient on every significand pair)
+#ifndef QEC_DIV4
+#define QEC_DIV4 0
+#endif
 __device__ __forceinline__ float div_short(float n, float d)
 {
+    if constexpr (QEC_DIV4) {
+        const float y = __builtin_amdgcn_rcpf(d);
+        const float q = n * y;
+        return __builtin_fmaf(__builtin_fmaf(-d, q, n), y, q);
+    }
     const float y0 = __builtin_amdgcn_rcpf(d);
     const float e = __builtin_fmaf(-d, y0, 1.0f);
     const float y1 = __builtin_fmaf(e, y0, y0);
@@ -1572,7 +1583,7 @@ void bp_decode_kernel(const BpArgs a)
     __shared__ __attribute__((aligned(8))) uint8_t stage_all[waves_per_block<TU>() * kStage];
     uint8_t* stage = stage_all + (threadIdx.x >> 6) * kStage;
     if constexpr (MODE == 2) {
-        const long long nX = a.counts[0], nZ = a.counts[1];
+        const long long nX = a.counts[0], nZ = a.counts[a.countStride];
         const long long wXn = (nX + G - 1) / G, wTot = wXn + (nZ + G - 1) / G;
         const long long nw = (long long)gridDim.x * (blockDim.x >> 6);
         // software pipelined: the list entry two sectors ahead and the syndrome bits of the next one
@@ -2010,7 +2021,7 @@ bool decode_pattern_masks(const void* variant, float errorProbability, uint32_t 
 int launch_decode_list(const void* variant, const Code& c, const uint8_t* sX, const uint8_t* sZ, long long B,
                        float errorProbability, int maxIter, int hardPaths, uint8_t* rec, int32_t* iters,
                        uint32_t* merge, const int32_t* listX, const int32_t* listZ, const uint32_t* counts,
-                       hipStream_t stream, int rec_stride, bool merge_only)
+                       hipStream_t stream, int rec_stride, bool merge_only, int count_stride)
 {
     const Variant* v = static_cast<const Variant*>(variant);
     if (!v->list) return fail(QEC_ERR_UNSUPPORTED, "bp_decode: no list-mode kernel for this code");
@@ -2021,6 +2032,7 @@ int launch_decode_list(const void* variant, const Code& c, const uint8_t* sX, co
     a.wX = (c.mX + 31) / 32; a.wZ = (c.mZ + 31) / 32;
     a.rec = rec; a.iters = iters; a.merge = merge;
     a.listX = listX; a.listZ = listZ; a.counts = counts; a.mergeOnly = merge_only ? 1 : 0;
+    a.countStride = count_stride;
     a.B = B; a.P = c.P; a.G = 64 / c.P;
     a.n = c.n; a.mX = c.mX; a.mZ = c.mZ;
     a.nb = (c.n + 7) / 8; a.recBytes = rec_stride > 0 ? rec_stride : 2 * a.nb + 1;

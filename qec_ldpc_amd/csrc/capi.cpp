@@ -30,7 +30,7 @@ bool decode_pattern_masks(const void* variant, float errorProbability, uint32_t 
 int launch_decode_list(const void* variant, const Code& c, const uint8_t* sX, const uint8_t* sZ, long long B,
                        float errorProbability, int maxIter, int hardPaths, uint8_t* rec, int32_t* iters,
                        uint32_t* merge, const int32_t* listX, const int32_t* listZ, const uint32_t* counts,
-                       hipStream_t stream, int rec_stride, bool merge_only);
+                       hipStream_t stream, int rec_stride, bool merge_only, int count_stride);
 bool triage_supported(const Code& c);
 bool triage_aligned(const void* sX, const void* sZ);
 int launch_triage(const Code& c, const uint32_t* sX, const uint32_t* sZ, long long B, const uint32_t pats[4],
@@ -45,7 +45,10 @@ bool mc_fused_supported(const Code& c, int rec_stride);
 int launch_mc_fused(const Code& c, uint64_t seed, uint64_t start, long long B, float p, const uint32_t pats[4],
                     uint32_t* sX, uint32_t* sZ, uint8_t* rec, int rec_stride, int32_t* iters, uint32_t* merge,
                     int32_t* listX, int32_t* listZ, int32_t* listS, uint32_t* counts, const uint64_t* imp_cols,
-                    unsigned long long* counters, bool survivors, hipStream_t st);
+                    unsigned long long* counters, unsigned long long* partials, bool survivors, hipStream_t st);
+long long mc_fused_parts(long long B);
+int mc_fused_count_words();
+int mc_fused_count_stride();
 int launch_statistics_packed(const Code& c, const uint64_t* imp_cols, const uint8_t* errp, int estride, const uint8_t* rec,
                              const int32_t* iters, long long B, unsigned long long* counters, hipStream_t st,
                              int rec_stride = 0);
@@ -127,6 +130,7 @@ struct qec_decoder {
     DeviceArray<uint8_t> msX, msZ, merrp, mrec, mtype;
     DeviceArray<int32_t> mit, midx;
     DeviceArray<unsigned long long> mcount;
+    DeviceArray<unsigned long long> mpart;  // fused Monte-Carlo kernel: per-workgroup counter sums
     EventSet mc_ev;  // qec_monte_carlo's ring of decode-time event pairs
     // multi-device group (qec_decoder_create_multi): the parts do the work, this handle only routes
     std::vector<qec_decoder*> parts;
@@ -592,7 +596,7 @@ int dispatch_decode(qec_decoder* d, const uint8_t* sX, const uint8_t* sZ, long l
                            iters, d->merge.data(), lX, lZ, cnt, st, rec_stride);
         if (!rc)
             rc = launch_decode_list(d->variant, c, sX, sZ, B, p, maxIter, hp, rec, iters, d->merge.data(), lX, lZ, cnt, st,
-                                    rec_stride, false);
+                                    rec_stride, false, 1);
         if (rc) return rc;
         return ws_release(d, st);
     }
@@ -842,7 +846,8 @@ int mc_batch(qec_decoder* d, McArgsHost h, int src, float p, int maxIter, int st
         int rc = ws_acquire(d, st);
         if (rc) return rc;
         if ((rc = ws_reserve(d->merge, (size_t)B, st, "monte carlo")) ||
-            (rc = ws_reserve(d->tlist, 3 * (size_t)B + 3, st, "monte carlo")))
+            (rc = ws_reserve(d->tlist, 3 * (size_t)B + mc_fused_count_words(), st, "monte carlo")) ||
+            (rc = ws_reserve(d->mpart, (size_t)mc_fused_parts(B) * QEC_MC_NCOUNTERS_ALL, st, "monte carlo")))
             return rc;
         int32_t* lX = d->tlist.data();
         int32_t* lZ = lX + B;
@@ -850,17 +855,19 @@ int mc_batch(qec_decoder* d, McArgsHost h, int src, float p, int maxIter, int st
         uint32_t* cnt = reinterpret_cast<uint32_t*>(lS + B);
         uint32_t* sXp = reinterpret_cast<uint32_t*>(d->msX.data());
         uint32_t* sZp = reinterpret_cast<uint32_t*>(d->msZ.data());
-        QEC_HIP_CHECK(hipMemsetAsync(cnt, 0, 3 * sizeof(uint32_t), st));
+        QEC_HIP_CHECK(hipMemsetAsync(cnt, 0, mc_fused_count_words() * sizeof(uint32_t), st));
         if (ev0) QEC_HIP_CHECK(hipEventRecord(ev0, st));
         for (int pass = 0; pass < 2; ++pass) {
             if (pass == 1) {
                 rc = launch_decode_list(d->variant, c, d->msX.data(), d->msZ.data(), B, p, maxIter, hard_path_bits(d),
-                                        d->mrec.data(), d->mit.data(), d->merge.data(), lX, lZ, cnt, st, rstride, true);
+                                        d->mrec.data(), d->mit.data(), d->merge.data(), lX, lZ, cnt, st, rstride, true,
+                                        mc_fused_count_stride());
                 if (rc) return rc;
                 if (ev1) QEC_HIP_CHECK(hipEventRecord(ev1, st));
             }
             rc = launch_mc_fused(c, h.seed, h.start, B, h.p, pats, sXp, sZp, d->mrec.data(), rstride, d->mit.data(),
-                                 d->merge.data(), lX, lZ, lS, cnt, d->imp_cols.data(), d->mcount.data(), pass == 1, st);
+                                 d->merge.data(), lX, lZ, lS, cnt, d->imp_cols.data(), d->mcount.data(), d->mpart.data(),
+                                 pass == 1, st);
             if (rc) return rc;
         }
         return ws_release(d, st);

@@ -382,8 +382,15 @@ __global__ __launch_bounds__(64 * kTriageWaves) void triage_kernel(const TriageA
 //      written as the triage kernel writes them, it is appended to listX / listZ for the sectors that
 //      go on and to listS, and mc_survivor_kernel counts it after the list-mode decode.
 // withX / withZ (errors present) are counted here for every sample.
-constexpr int kFusedWaves = 4;
+// 16-wave workgroups: the workgroup-level atomics (list appends) are few, and the counters go to
+// per-workgroup partial sums (mc_reduce_kernel) -- same-address atomics from every workgroup
+// serialise at L2 (one per workgroup and counter at 4-wave workgroups: ~37 k per 2^20 samples)
+#ifndef QEC_FUSED_WAVES
+#define QEC_FUSED_WAVES 16
+#endif
+constexpr int kFusedWaves = QEC_FUSED_WAVES;
 constexpr int kHitCap = 16;  // hits a lane keeps (P61 at p = 0.01: 6.1 on average)
+constexpr int kCountStride = 32;  // words between the three list lengths (separate L2 lines)
 
 struct FusedArgs {
     GapParams gp;
@@ -399,11 +406,58 @@ struct FusedArgs {
     int32_t* listX;
     int32_t* listZ;
     int32_t* listS;
-    uint32_t* counts;  // [3]: listX, listZ, listS lengths (zeroed before the launch)
+    uint32_t* counts;  // listX, listZ, listS lengths at [0], [kCountStride], [2 kCountStride] (zeroed first)
     const uint64_t* imp_cols;
     int imp_cw;
     unsigned long long* counters;  // [C_N + 2] (iteration sums at C_N, C_N + 1)
+    unsigned long long* partials;  // [fused grid][C_N + 2]: mc_fused_kernel's per-workgroup sums
+    int nparts;                    // its grid size
 };
+
+// the workgroup's counters (each wave's ballot popcounts) stored as its row of partials
+template <int NWAVES>
+__device__ __forceinline__ void store_partials(const unsigned long long (&c)[C_N + 2], unsigned long long (*part)[C_N + 2],
+                                               unsigned long long* __restrict__ partials)
+{
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    if (lane < C_N + 2) {
+        unsigned long long v = 0;
+#pragma unroll
+        for (int k = 0; k < C_N + 2; ++k) v = lane == k ? c[k] : v;
+        part[wv][lane] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < C_N + 2) {
+        unsigned long long v = 0;
+        for (int w = 0; w < NWAVES; ++w) v += part[w][threadIdx.x];
+        partials[(size_t)blockIdx.x * (C_N + 2) + threadIdx.x] = v;
+    }
+}
+
+// one workgroup: the partial sums of mc_fused_kernel added to the counters (C_N + 2 atomics)
+__global__ __launch_bounds__(256) void mc_reduce_kernel(const unsigned long long* __restrict__ partials, int nparts,
+                                                        unsigned long long* __restrict__ counters)
+{
+    __shared__ unsigned long long acc[256 / 64][C_N + 2];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    unsigned long long v[C_N + 2] = {};
+    for (int w = threadIdx.x; w < nparts; w += blockDim.x)
+#pragma unroll
+        for (int k = 0; k < C_N + 2; ++k) v[k] += partials[(size_t)w * (C_N + 2) + k];
+#pragma unroll
+    for (int k = 0; k < C_N + 2; ++k)
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) v[k] += __shfl_xor(v[k], o);
+    if (lane == 0)
+#pragma unroll
+        for (int k = 0; k < C_N + 2; ++k) acc[wv][k] = v[k];
+    __syncthreads();
+    if (threadIdx.x < C_N + 2) {
+        unsigned long long t = 0;
+        for (int w = 0; w < 256 / 64; ++w) t += acc[w][threadIdx.x];
+        if (t) atomicAdd(&counters[threadIdx.x], t);
+    }
+}
 
 // Decision bits of this lane's sample in the record layout (x bits at [0, 8 nb), z at [8 nb, 16 nb)), as
 // u32 words [0, 2 NW) with the flags byte left 0, XOR its hits: the residual the I-P check takes.
@@ -569,7 +623,7 @@ __global__ __launch_bounds__(64 * kFusedWaves) void mc_fused_kernel(const FusedA
     if (threadIdx.x < 3) {
         uint32_t tot = 0;
         for (int w = 0; w < kFusedWaves; ++w) tot += wcnt[w][threadIdx.x];
-        wgbase[threadIdx.x] = tot ? atomicAdd(&a.counts[threadIdx.x], tot) : 0u;
+        wgbase[threadIdx.x] = tot ? atomicAdd(&a.counts[threadIdx.x * kCountStride], tot) : 0u;
     }
     __syncthreads();
     uint32_t base[3] = {wgbase[0], wgbase[1], wgbase[2]};
@@ -578,7 +632,7 @@ __global__ __launch_bounds__(64 * kFusedWaves) void mc_fused_kernel(const FusedA
     if ((gx >> lane) & 1ull) a.listX[base[0] + __popcll(gx & lt)] = (int32_t)b;
     if ((gz >> lane) & 1ull) a.listZ[base[1] + __popcll(gz & lt)] = (int32_t)b;
     if ((gs >> lane) & 1ull) a.listS[base[2] + __popcll(gs & lt)] = (int32_t)b;
-    flush_counters<kFusedWaves>(c, part, a.counters);
+    store_partials<kFusedWaves>(c, part, a.partials);
 }
 
 // The survivors' counters after the list-mode decode: lane per listed sample (grid-stride over
@@ -599,7 +653,7 @@ __global__ __launch_bounds__(64 * kSurvWaves) void mc_survivor_kernel(const Fuse
     __shared__ uint32_t region[64 * kSurvWaves * RS];
     __shared__ unsigned long long sres[kSurvWaves][NW];
     __shared__ unsigned long long part[kSurvWaves][C_N + 2];
-    const long long cnt = a.counts[2];
+    const long long cnt = a.counts[2 * kCountStride];
     if ((long long)blockIdx.x * blockDim.x >= cnt) return;  // workgroup-uniform: no survivor for this one
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     gap_table(a.gp, n, T);
@@ -731,6 +785,12 @@ static bool fused_fns(const Code& c, FusedFn& fused, FusedFn& surv)
     return true;
 }
 
+// workgroups of the fused kernel for a batch of B samples (rows of the partials workspace); the
+// list lengths' words (counts) span mc_fused_count_words()
+long long mc_fused_parts(long long B) { return (B + 64LL * kFusedWaves - 1) / (64LL * kFusedWaves); }
+int mc_fused_count_words() { return 2 * kCountStride + 1; }
+int mc_fused_count_stride() { return kCountStride; }
+
 bool mc_fused_supported(const Code& c, int rec_stride)
 {
     FusedFn f, s;
@@ -743,7 +803,7 @@ bool mc_fused_supported(const Code& c, int rec_stride)
 int launch_mc_fused(const Code& c, uint64_t seed, uint64_t start, long long B, float p, const uint32_t pats[4],
                     uint32_t* sX, uint32_t* sZ, uint8_t* rec, int rec_stride, int32_t* iters, uint32_t* merge,
                     int32_t* listX, int32_t* listZ, int32_t* listS, uint32_t* counts, const uint64_t* imp_cols,
-                    unsigned long long* counters, bool survivors, hipStream_t st)
+                    unsigned long long* counters, unsigned long long* partials, bool survivors, hipStream_t st)
 {
     FusedFn fused = nullptr, surv = nullptr;
     if (!mc_fused_supported(c, rec_stride) || !fused_fns(c, fused, surv))
@@ -756,9 +816,12 @@ int launch_mc_fused(const Code& c, uint64_t seed, uint64_t start, long long B, f
     a.sX = sX; a.sZ = sZ; a.rec = rec; a.iters = iters; a.merge = merge;
     a.listX = listX; a.listZ = listZ; a.listS = listS; a.counts = counts;
     a.imp_cols = imp_cols; a.imp_cw = c.imp_col_words; a.counters = counters;
+    a.partials = partials; a.nparts = (int)mc_fused_parts(B);
     if (!survivors) {
-        const long long per = 64LL * kFusedWaves;
-        hipLaunchKernelGGL(fused, dim3((unsigned)((B + per - 1) / per)), dim3(64 * kFusedWaves), 0, st, a);
+        hipLaunchKernelGGL(fused, dim3((unsigned)a.nparts), dim3(64 * kFusedWaves), 0, st, a);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return fail(QEC_ERR_HIP, std::string("mc fused launch: ") + hipGetErrorString(e));
+        hipLaunchKernelGGL(mc_reduce_kernel, dim3(1), dim3(256), 0, st, partials, a.nparts, counters);
     } else {
         int dev = 0, cus = 256;
         if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||

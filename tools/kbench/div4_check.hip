@@ -6,7 +6,7 @@
 // [1, 2): 2^46 pairs; scaling n or d by a power of two scales q0, r and q1 exactly while everything
 // stays normal, so these pairs stand for the whole normal domain of the scaled folds), after
 // checking that v_rcp_f32 itself is exponent-independent there (rcp(m 2^e) == rcp(m) 2^-e for every
-// significand m and e in [-70, 40]).  Prints one JSON line; any mismatch rules the candidate out.
+// significand m and e in [-100, 40], the guarded and the scaled domains).  Prints one JSON line; any mismatch rules the candidate out.
 //   hipcc --offload-arch=gfx950 -O3 -ffp-contract=off tools/kbench/div4_check.hip -o tools/kbench/div4_check
 #include <hip/hip_runtime.h>
 
@@ -24,7 +24,7 @@ __device__ __forceinline__ float div4(float n, float d)
     return __builtin_fmaf(r, y0, q0);
 }
 
-// part 1: thread per significand m of d; rcp(m 2^e) against rcp(m) 2^-e for e in [-70, 40]
+// part 1: thread per significand m of d; rcp(m 2^e) against rcp(m) 2^-e for e in [-100, 40]
 __global__ void rcp_scale_kernel(unsigned long long* bad)
 {
     const uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
@@ -32,7 +32,7 @@ __global__ void rcp_scale_kernel(unsigned long long* bad)
     const float d1 = __uint_as_float((127u << 23) | m);
     const uint32_t y1 = __float_as_uint(__builtin_amdgcn_rcpf(d1));
     unsigned long long nb = 0;
-    for (int e = -70; e <= 40; ++e) {
+    for (int e = -100; e <= 40; ++e) {
         const float d = __uint_as_float(((uint32_t)(127 + e) << 23) | m);
         const uint32_t y = __float_as_uint(__builtin_amdgcn_rcpf(d));
         // y1 2^-e: the exponent field moves by -e (y1 is in (0.5, 1], its scaled value stays normal)

@@ -170,7 +170,8 @@ int qec_decoder_device(const qec_decoder* dec);         /* HIP device ordinal (o
  *     4096 <= B <= 2^22 (codes with one syndrome per wave, P > 32: 4096 <= B <= 2^19, above which
  *     the pass costs more than it saves), 2 = sorted when B <= 2^22, 3 = as 2 but with the one-launch
  *     local order for B <= 2^18 short-row codes (each chunk sorted in LDS, chunks interleaved by rank;
- *     measured slower than the global sort at P7 65 536, kept for experiments).  The workspace (5 B per syndrome + 1 MiB) is allocated
+ *     measured slower than the global sort at P7 65 536, kept for experiments), 4 = as 2 but the
+ *     global sort in one launch with a software grid barrier for up to 128 chunks (measured slower).  The workspace (5 B per syndrome + 1 MiB) is allocated
  *     by qec_decoder_create for max_batch and grown on demand by larger calls.
  *   QEC_OPT_SECTOR_SPLIT (default 1): the X and Z sectors of a syndrome are decoded by two
  *     waves instead of one after the other (halves the longest wave).  The launch then zeroes

@@ -216,6 +216,15 @@ struct Tune {
 #ifndef QEC_LIST_AGREE
 #define QEC_LIST_AGREE 0
 #endif
+//   QEC_LIST_PREFETCH      list mode: the next sector's list entry and syndrome bits loaded ahead (measured:
+//                          no gain at p = 2e-3 / 5e-3, -3 % at 1e-2; off)
+//   QEC_LIST_MERGE_ONLY    list mode of the fused Monte-Carlo pipeline: flags into the merge word only
+#ifndef QEC_LIST_PREFETCH
+#define QEC_LIST_PREFETCH 0
+#endif
+#ifndef QEC_LIST_MERGE_ONLY
+#define QEC_LIST_MERGE_ONLY 1
+#endif
 // The list-mode (MODE 2) tuning of a variant: its own occupancy and the agreement test with the cycle
 // jump under the syndrome stop (see kAgree).
 template <class TU, int LW>
@@ -502,18 +511,12 @@ __device__ __forceinline__ bool band(bool a, bool b) { return (int)a & (int)b; }
 //   (profiles/r01/session5/div_check.json).
 // The guard below is evaluated for a whole column of divisions and the short path taken only
 // when every live lane of the wave passes it; otherwise the full sequence runs.
-//   QEC_DIV4  experiment: the short form without the reciprocal refinement (4 instructions; valid only if
-//             tools/kbench/div4_check.hip finds it equal to the IEEE quotient on every significand pair)
-#ifndef QEC_DIV4
-#define QEC_DIV4 0
-#endif
+// (Without the refinement -- q0 = n rcp(d), one residual correction with rcp(d) -- the form is 4
+// instructions and would take 9 % of a soft iteration's VALU, but it is not correctly rounded:
+// tools/kbench/div4_check.hip finds 47 045 of the 2^46 significand pairs differing from the IEEE
+// quotient.)
 __device__ __forceinline__ float div_short(float n, float d)
 {
-    if constexpr (QEC_DIV4) {
-        const float y = __builtin_amdgcn_rcpf(d);
-        const float q = n * y;
-        return __builtin_fmaf(__builtin_fmaf(-d, q, n), y, q);
-    }
     const float y0 = __builtin_amdgcn_rcpf(d);
     const float e = __builtin_fmaf(-d, y0, 1.0f);
     const float y1 = __builtin_fmaf(e, y0, y0);
@@ -1586,6 +1589,16 @@ void bp_decode_kernel(const BpArgs a)
         const long long nX = a.counts[0], nZ = a.counts[a.countStride];
         const long long wXn = (nX + G - 1) / G, wTot = wXn + (nZ + G - 1) / G;
         const long long nw = (long long)gridDim.x * (blockDim.x >> 6);
+        if constexpr (!QEC_LIST_PREFETCH) {
+            for (long long vw = wave; vw < wTot; vw += nw) {
+                const bool doX = vw < wXn;  // wave-uniform
+                const long long slot = (doX ? vw : vw - wXn) * G + g;
+                const bool in_range = (g < G) && (slot < (doX ? nX : nZ));
+                const uint32_t b = in_range ? (uint32_t)(doX ? a.listX : a.listZ)[slot] : 0u;
+                decode_group<RX, RZ, L, STOP, SH, TU, 2>(a, tab0, stage, i, gb, b, in_range, doX);
+            }
+            return;
+        }
         // software pipelined: the list entry two sectors ahead and the syndrome bits of the next one
         // are in flight while a sector decodes (each is otherwise a dependent global load at its start)
         Lane lq{i, gb, 0, 0, false};
@@ -1649,7 +1662,13 @@ using ShiftsP61 = GeneratedShifts<4, 5, 10, 61, 9, 49, TuneP61::kRelabel, TuneP6
 #ifndef QEC_P7_MINW
 #define QEC_P7_MINW 8
 #endif
-using TuneP7 = Tune<QEC_P7_MINW, true, false, true, true, true, false, 2, 1, 7, 3>;
+#ifndef QEC_P7_MWX
+#define QEC_P7_MWX 0
+#endif
+#ifndef QEC_P7_MWZ
+#define QEC_P7_MWZ 0
+#endif
+using TuneP7 = Tune<QEC_P7_MINW, true, false, true, true, true, false, 2, 1, 7, 3, false, QEC_P7_MWX, QEC_P7_MWZ>;
 struct TuneP7MinReg : TuneP7 {};
 using ShiftsP7 = GeneratedShifts<3, 3, 6, 7, 2, 3, TuneP7::kRelabel, TuneP7::kMaskSelect>;
 #ifndef QEC_P61_MINREG
@@ -2031,7 +2050,7 @@ int launch_decode_list(const void* variant, const Code& c, const uint8_t* sX, co
     a.sX = sX; a.sZ = sZ; a.sbits = 1;
     a.wX = (c.mX + 31) / 32; a.wZ = (c.mZ + 31) / 32;
     a.rec = rec; a.iters = iters; a.merge = merge;
-    a.listX = listX; a.listZ = listZ; a.counts = counts; a.mergeOnly = merge_only ? 1 : 0;
+    a.listX = listX; a.listZ = listZ; a.counts = counts; a.mergeOnly = QEC_LIST_MERGE_ONLY && merge_only ? 1 : 0;
     a.countStride = count_stride;
     a.B = B; a.P = c.P; a.G = 64 / c.P;
     a.n = c.n; a.mX = c.mX; a.mZ = c.mZ;

@@ -106,7 +106,7 @@ struct qec_decoder {
     std::string variant_name;
     int hard_paths = 1;             // QEC_OPT_HARD_PATHS
     int cycle_jump = 1;             // QEC_OPT_CYCLE_JUMP
-    int schedule = 1;               // QEC_OPT_SCHEDULE (0 off, 1 auto, 2 always, 3 always with the local order)
+    int schedule = 1;               // QEC_OPT_SCHEDULE (0 off, 1 auto, 2 always, 3 / 4 always, local / one-launch order)
     int sector_split = 1;           // QEC_OPT_SECTOR_SPLIT (0 off, 1 auto, 2 split waves, 3 sector launches)
     int phase_stats = 0;            // QEC_OPT_PHASE_STATS
     int triage = 1;                 // QEC_OPT_TRIAGE
@@ -480,7 +480,7 @@ int qec_decoder_set_option(qec_decoder* d, int option, int value)
     case QEC_OPT_HARD_PATHS: d->hard_paths = value != 0; return QEC_OK;
     case QEC_OPT_CYCLE_JUMP: d->cycle_jump = value != 0; return QEC_OK;
     case QEC_OPT_SCHEDULE:
-        if (value < 0 || value > 3) return fail(QEC_ERR_ARG, "qec_decoder_set_option: QEC_OPT_SCHEDULE is 0 .. 3");
+        if (value < 0 || value > 4) return fail(QEC_ERR_ARG, "qec_decoder_set_option: QEC_OPT_SCHEDULE is 0 .. 4");
         d->schedule = value;
         return QEC_OK;
     case QEC_OPT_SECTOR_SPLIT:
@@ -612,7 +612,7 @@ int dispatch_decode(qec_decoder* d, const uint8_t* sX, const uint8_t* sZ, long l
             return rc;
         int32_t* pm = nullptr;
         // a sector-split launch merges its flags in zeroed words: the order pass zeroes them
-        const int method = d->schedule == 3 ? QEC_ORDER_LOCAL : QEC_ORDER_GLOBAL;
+        const int method = d->schedule == 3 ? QEC_ORDER_LOCAL : d->schedule == 4 ? QEC_ORDER_ONE_LAUNCH : QEC_ORDER_GLOBAL;
         rc = launch_schedule(sX, sZ, sbits, B, c.mX, c.mZ, d->sched.data(), split ? d->merge.data() : nullptr, &pm, st,
                              method, d->gbar.data());
         if (rc) return rc;

@@ -11,9 +11,10 @@ namespace qec {
 
 // BpArgs::hardPaths bits (from QEC_OPT_HARD_PATHS / QEC_OPT_CYCLE_JUMP)
 enum { QEC_HP_FORMS = 1, QEC_HP_CYCLE = 2, QEC_HP_PHASE = 4 /* launch the instrumented kernel */ };
-// dispatch-order method (schedule.hip, launch_schedule): the global counting sort, or the one-launch
-// chunk-local order (measured slower; experiments)
-enum { QEC_ORDER_GLOBAL = 0, QEC_ORDER_LOCAL = 1 };
+// dispatch-order method (schedule.hip, launch_schedule): the global counting sort, the one-launch
+// chunk-local order or the global sort in one launch with a software grid barrier (both measured
+// slower; experiments)
+enum { QEC_ORDER_GLOBAL = 0, QEC_ORDER_LOCAL = 1, QEC_ORDER_ONE_LAUNCH = 2 };
 
 // Thread-local last-error text behind qec_last_error().
 void set_error(const std::string& msg);

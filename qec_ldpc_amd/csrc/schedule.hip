@@ -289,10 +289,10 @@ __global__ __launch_bounds__(kScatThreads) void schedule_scatter_fused_kernel(co
 // workgroup of the grid is resident and the barrier cannot wait on one that was never scheduled.
 // bar[0] counts arrivals; bar[1] departures, and the last workgroup to leave zeroes both for the next
 // launch (bar comes zeroed from qec_decoder_create; graph replays reuse it the same way).
+// Measured slower than the two launches it replaces (P7 65 536: 0.082 vs 0.070 ms per decode call,
+// profiles/r04/cmp_one_launch_order_p7.txt): the arrival polling costs more than the launch gap.
+// Kept as QEC_OPT_SCHEDULE = 4 for experiments.
 constexpr int kOneLaunchChunks = 128;
-#ifndef QEC_SCHED_ONE_LAUNCH
-#define QEC_SCHED_ONE_LAUNCH 1
-#endif
 
 __device__ __forceinline__ void grid_arrive_wait(uint32_t* bar, uint32_t nblocks)
 {
@@ -478,7 +478,7 @@ int launch_schedule(const uint8_t* sX, const uint8_t* sZ, bool sbits, long long 
     // buckets: weights 0 .. mX + mZ (fused pass), 256 for the separate offsets / scatter passes
     int nbk = kBuckets;
     if (fused && mX + mZ + 1 < kBuckets) nbk = mX + mZ + 1 < 32 ? 32 : mX + mZ + 1;
-    if (QEC_SCHED_ONE_LAUNCH && fused && bar != nullptr && nch <= kOneLaunchChunks) {
+    if (method == QEC_ORDER_ONE_LAUNCH && fused && bar != nullptr && nch <= kOneLaunchChunks) {
         // histogram, grid barrier, offsets and scatter in one launch (schedule_one_launch_kernel)
         if (sbits)
             hipLaunchKernelGGL(schedule_one_launch_kernel<2>, dim3(nch), dim3(kScatThreads), 0, st, sX, sZ, B,

@@ -234,7 +234,7 @@ def test_cycle_jump_bit_identical(env, key, N):
 
 
 @pytest.mark.parametrize("key", ["P7", "P61"])
-@pytest.mark.parametrize("schedule,split", [(0, 0), (0, 2), (2, 0), (2, 2), (3, 0), (3, 2), (0, 3), (2, 3)])
+@pytest.mark.parametrize("schedule,split", [(0, 0), (0, 2), (2, 0), (2, 2), (3, 0), (3, 2), (0, 3), (2, 3), (4, 0), (4, 2)])
 @pytest.mark.parametrize("B", [1, 2, 383])
 def test_schedule_and_split_bit_identical(env, key, schedule, split, B):
     """QEC_OPT_SCHEDULE (waves take syndromes heaviest-first, schedule.hip) and
@@ -422,3 +422,29 @@ def test_non_binary_syndrome_entries(env, key, engine, stop):
         if want_q:
             assert same_floats(g[4], o[4])
     assert (g[2][(sX > 1).any(1)] & 1).all()
+
+
+@pytest.mark.parametrize("key,B", [("P7", 65536), ("P7", 5000), ("P61", 65536)])
+def test_one_launch_order_repeated(env, key, B):
+    """QEC_OPT_SCHEDULE = 4: the dispatch order in one launch with a software grid barrier (schedule.hip,
+    schedule_one_launch_kernel; its barrier words must come back zeroed after every launch): five
+    calls in a row give the records of the unordered decode."""
+    import torch
+    code, dec, _ = env[key]
+    x, z = depolarizing_errors(code.n, 99 + B, B, 0.02)
+    dev = torch.device("cuda", 0)
+    tX = torch.from_numpy(code.syndrome(0, x)).to(dev)
+    tZ = torch.from_numpy(code.syndrome(1, z)).to(dev)
+    outs = []
+    try:
+        for sched in (0, 4, 4, 4, 4, 4):
+            dec.set_option("schedule", sched)
+            rec = torch.empty((B, dec.record_bytes()), dtype=torch.uint8, device=dev)
+            its = torch.empty((B, 2), dtype=torch.int32, device=dev)
+            dec.decode_batch_packed_dev(tX, tZ, 0.02, 20, "fixed", rec, its)
+            torch.cuda.synchronize()
+            outs.append((rec.cpu().numpy(), its.cpu().numpy()))
+    finally:
+        dec.set_option("schedule", 1)
+    for r, it in outs[1:]:
+        assert np.array_equal(r, outs[0][0]) and np.array_equal(it, outs[0][1])

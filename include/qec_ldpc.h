@@ -176,8 +176,9 @@ int qec_decoder_device(const qec_decoder* dec);         /* HIP device ordinal (o
  *   QEC_OPT_SECTOR_SPLIT (default 1): the X and Z sectors of a syndrome are decoded by two
  *     waves instead of one after the other (halves the longest wave).  The launch then zeroes
  *     flags[] first and each sector ORs in its bits.  Bit-identical either way.  0 = off,
- *     1 = the kernel variant's measured choice, 2 = on where the variant has split kernels (the
- *     two shipped codes), 3 = sector launches: two launches on the caller's stream, sector X then
+ *     1 = the kernel variant's measured choice (P7: split waves below 2^19 syndromes; P61: sector
+ *     launches from 2^18 on), 2 = on where the variant has split kernels (the two shipped codes),
+ *     3 = sector launches: two launches on the caller's stream, sector X then
  *     sector Z, each kernel compiled (and its registers allocated) for its own sector only; the Z
  *     launch ORs its flags into the byte the X launch stored (shipped codes; elsewhere as 0).
  *   QEC_OPT_PHASE_STATS (default 0; measurement only, shipped codes): launches an instrumented

@@ -1757,8 +1757,8 @@ struct Variant {
     const char* name;
     KernelFn list = nullptr;  // syndrome stop, list mode (MODE 2: the sectors the triage passed on)
     int min_waves_syn = 1;    // its occupancy (waves per SIMD), for the list launch's grid
-    KernelFn seq[3][2] = {};  // sector launches (MODE 3 / 4): [stop][sector]
-    bool seq_auto = false;    // QEC_OPT_SECTOR_SPLIT = 1 takes the sector launches
+    KernelFn seq[3][2] = {};     // sector launches (MODE 3 / 4): [stop][sector]
+    long long seq_min_batch = 0;  // QEC_OPT_SECTOR_SPLIT = 1 takes the sector launches from this batch on (0: never)
 };
 
 // Both sectors' iteration-0 tables on the host, entry for entry what the device's table0_entry
@@ -1844,6 +1844,9 @@ static Variant gen_p61()
             if (stop != QEC_STOP_SYNDROME)
                 for (int sec = 0; sec < 2; ++sec) v.seq[stop][sec] = p61_minreg_seq_kernel(stop, sec);
         }
+        // sector launches from 2^18 syndromes on: +1.3 % at 262 144, +0.3 % at 524 288, +1.9 % at 2^20,
+        // but -2.7 % at 131 072 and -10 % at 65 536 (a second launch tail; profiles/r04/cmp_sector_launch_*.txt)
+        v.seq_min_batch = 1LL << 18;
     }
     return v;
 }
@@ -1910,17 +1913,18 @@ const void* select_variant(const Code& c, std::string& name)
 // 2^20 1790 vs 1835 M/s split vs one wave per group; profiles/r02/p7_split_r02s3zz.txt).
 constexpr long long kSplitAutoMaxBatch = 1LL << 19;
 
-// Sector launches (QEC_OPT_SECTOR_SPLIT = 3, or 1 where the variant's measured choice, seq_auto):
+// Sector launches (QEC_OPT_SECTOR_SPLIT = 3, or 1 from the variant's seq_min_batch on):
 // two launches, sector X then sector Z, each kernel compiled for its own sector (no merge words).
-static bool decode_uses_seq(const Variant* v, int stop, int split)
+static bool decode_uses_seq(const Variant* v, int stop, int split, long long B)
 {
-    return (split == 3 || (split == 1 && v->seq_auto)) && v->seq[stop][0] != nullptr && v->seq[stop][1] != nullptr;
+    return (split == 3 || (split == 1 && v->seq_min_batch > 0 && B >= v->seq_min_batch)) && v->seq[stop][0] != nullptr &&
+           v->seq[stop][1] != nullptr;
 }
 
 bool decode_uses_split(const void* variant, int stop, int split, long long B)
 {
     const Variant* v = static_cast<const Variant*>(variant);
-    if (decode_uses_seq(v, stop, split)) return false;
+    if (decode_uses_seq(v, stop, split, B)) return false;
     return (split == 2 || (split == 1 && v->split_auto && B < kSplitAutoMaxBatch)) && v->split[stop] != nullptr;
 }
 
@@ -1969,7 +1973,7 @@ int launch_decode(const void* variant, const Code& c, const uint8_t* sX, const u
     relabel(c.EX.data(), c.J, c.L, c.P, v->relabel, a.SX, a.DX, a.CX);
     relabel(c.EZ.data(), c.K, c.L, c.P, v->relabel, a.SZ, a.DZ, a.CZ);
     const int wavesPerBlock = v->waves_per_block;
-    const bool seq = !phase && !split && decode_uses_seq(v, stop, split_opt);
+    const bool seq = !phase && !split && decode_uses_seq(v, stop, split_opt, B);
     const long long waves = (B + a.G - 1) / a.G * (split ? 2 : 1);
     const long long blocks = (waves + wavesPerBlock - 1) / wavesPerBlock;
     if (blocks > 0x7fffffffLL) return fail(QEC_ERR_ARG, "batch too large for one launch");

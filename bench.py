@@ -77,12 +77,12 @@ def lane_ops_per_syndrome(code, iters):
     ('Roofline'): per check (dc = L) L fma(1-2q), 2(L-2) prefix/first-slot
     muls, (L-1)(L-2)/2 leave-one-out muls, L output fmas, 1 select; per variable
     (dv = R) R subs, 2(R-1) prefix and R(R-1) leave-one-out muls, R adds and R
-    correctly rounded divisions of 11 instructions."""
+    correctly rounded divisions of 6 instructions (the kernel's short form)."""
     L = code.L
     chk = L + 2 * (L - 2) + (L - 1) * (L - 2) // 2 + L + 1
 
     def var(R):
-        return R + 2 * (R - 1) + R * (R - 1) + R + 11 * R
+        return R + 2 * (R - 1) + R * (R - 1) + R + 6 * R
 
     per_iter = (code.numEqsX + code.numEqsZ) * chk + code.n * (var(code.J) + var(code.K))
     return per_iter * iters

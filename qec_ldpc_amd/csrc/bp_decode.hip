@@ -1485,9 +1485,9 @@ constexpr int waves_per_block() { return QEC_WAVES_PER_BLOCK > 0 ? QEC_WAVES_PER
 // decode, then the flags byte and iteration counts.  MODE (see bp_decode_kernel) 0: both sectors,
 // plain store of the flags; 1 / 2: one sector, the two meet in the syndrome's merge word (atomicOr of
 // flags plus a done bit; the second to arrive stores the merged byte); 3: sector X of a sector launch
-// (stores its flags), 4: sector Z of a sector launch, enqueued after the X launch on the same stream
-// (ORs its flags into the byte the X launch stored).  Modes 3 and 4 compile one sector only, so each
-// kernel's registers are allocated for that sector alone.
+// (stores its flags in the syndrome's merge word), 4: sector Z of a sector launch, enqueued after the X
+// launch on the same stream (stores the flags byte: the merge word OR its own flags).  Modes 3 and 4
+// compile one sector only, so each kernel's registers are allocated for that sector alone.
 // pre: the sector's syndrome bits were loaded by the caller (sbPre; list mode, one sector per wave)
 template <int RX, int RZ, int L, int STOP, class SH, class TU, int MODE>
 __device__ __forceinline__ void decode_group(const BpArgs& a, const float* __restrict__ tab0, uint8_t* __restrict__ stage,
@@ -1519,10 +1519,12 @@ __device__ __forceinline__ void decode_group(const BpArgs& a, const float* __res
     }
     if (in_range && lane_i<SH>(ln) == 0) {
         uint8_t* fdst = a.rec != nullptr ? a.rec + b * (long long)a.recBytes + 2 * a.nb : a.flags + b;
-        if constexpr (MODE == 0 || MODE == 3) {
+        if constexpr (MODE == 0) {
             *fdst = (uint8_t)flags;
+        } else if constexpr (MODE == 3) {
+            a.merge[b] = flags;  // for the Z launch (a word per syndrome, not the record's byte: one line each)
         } else if constexpr (MODE == 4) {
-            *fdst = (uint8_t)(*fdst | flags);  // the X launch's byte (same stream, earlier launch)
+            *fdst = (uint8_t)(a.merge[b] | flags);  // the X launch's flags (same stream, earlier launch)
         } else if (MODE == 2 && a.mergeOnly) {
             // the fused Monte-Carlo pipeline reads the flags from the merge word itself
             // (mc_survivor_kernel): no returned value to wait for
@@ -1595,7 +1597,11 @@ void bp_decode_kernel(const BpArgs a)
                 const long long slot = (doX ? vw : vw - wXn) * G + g;
                 const bool in_range = (g < G) && (slot < (doX ? nX : nZ));
                 const uint32_t b = in_range ? (uint32_t)(doX ? a.listX : a.listZ)[slot] : 0u;
-                decode_group<RX, RZ, L, STOP, SH, TU, 2>(a, tab0, stage, i, gb, b, in_range, doX);
+                // laundered per sector: the rotation addresses derived from the lane index would otherwise
+                // be hoisted out of this loop into live registers (they spilled at 3 waves per SIMD)
+                int il = i, gbl = gb;
+                asm volatile("" : "+v"(il), "+v"(gbl));
+                decode_group<RX, RZ, L, STOP, SH, TU, 2>(a, tab0, stage, il, gbl, b, in_range, doX);
             }
             return;
         }
@@ -1913,12 +1919,19 @@ const void* select_variant(const Code& c, std::string& name)
 // 2^20 1790 vs 1835 M/s split vs one wave per group; profiles/r02/p7_split_r02s3zz.txt).
 constexpr long long kSplitAutoMaxBatch = 1LL << 19;
 
+bool decode_uses_split(const void* variant, int stop, int split, long long B);
 // Sector launches (QEC_OPT_SECTOR_SPLIT = 3, or 1 from the variant's seq_min_batch on):
 // two launches, sector X then sector Z, each kernel compiled for its own sector (no merge words).
 static bool decode_uses_seq(const Variant* v, int stop, int split, long long B)
 {
     return (split == 3 || (split == 1 && v->seq_min_batch > 0 && B >= v->seq_min_batch)) && v->seq[stop][0] != nullptr &&
            v->seq[stop][1] != nullptr;
+}
+
+bool decode_needs_merge(const void* variant, int stop, int split, long long B)
+{
+    const Variant* v = static_cast<const Variant*>(variant);
+    return decode_uses_seq(v, stop, split, B) || decode_uses_split(variant, stop, split, B);
 }
 
 bool decode_uses_split(const void* variant, int stop, int split, long long B)
@@ -1977,7 +1990,9 @@ int launch_decode(const void* variant, const Code& c, const uint8_t* sX, const u
     const long long waves = (B + a.G - 1) / a.G * (split ? 2 : 1);
     const long long blocks = (waves + wavesPerBlock - 1) / wavesPerBlock;
     if (blocks > 0x7fffffffLL) return fail(QEC_ERR_ARG, "batch too large for one launch");
-    if (seq) {  // sector X, then sector Z (which ORs its flags into X's byte) on the same stream
+    if (seq) {  // sector X, then sector Z (which merges X's flags from the merge words) on the same stream
+        if (merge == nullptr) return fail(QEC_ERR_ARG, "bp_decode: sector launches need the merge words");
+        a.merge = merge;
         for (int sec = 0; sec < 2; ++sec) {
             hipLaunchKernelGGL(v->seq[stop][sec], dim3((unsigned)blocks), dim3(64 * wavesPerBlock), 0, stream, a);
             hipError_t err = hipGetLastError();

@@ -25,6 +25,7 @@ long long schedule_local_max_batch();
 int launch_schedule(const uint8_t* sX, const uint8_t* sZ, bool sbits, long long B, int mX, int mZ, void* ws,
                     uint32_t* zero_merge, int32_t** perm_out, hipStream_t st, int method, uint32_t* bar);
 bool decode_uses_split(const void* variant, int stop, int split, long long B);
+bool decode_needs_merge(const void* variant, int stop, int split, long long B);
 bool decode_has_list(const void* variant);
 bool decode_pattern_masks(const void* variant, float errorProbability, uint32_t pats[4]);
 int launch_decode_list(const void* variant, const Code& c, const uint8_t* sX, const uint8_t* sZ, long long B,
@@ -601,7 +602,8 @@ int dispatch_decode(qec_decoder* d, const uint8_t* sX, const uint8_t* sZ, long l
         return ws_release(d, st);
     }
     const bool split = !d->phase_stats && decode_uses_split(d->variant, stop, d->sector_split, B);
-    if (split && (rc = ws_reserve(d->merge, (size_t)B, st, "decode"))) return rc;
+    const bool need_merge = !d->phase_stats && decode_needs_merge(d->variant, stop, d->sector_split, B);
+    if (need_merge && (rc = ws_reserve(d->merge, (size_t)B, st, "decode"))) return rc;
     const int32_t* perm = nullptr;
     bool zeroed = false;
     const bool single = 2 * c.P > 64;  // one syndrome per wave
@@ -620,7 +622,7 @@ int dispatch_decode(qec_decoder* d, const uint8_t* sX, const uint8_t* sZ, long l
         zeroed = split;
     }
     rc = launch_decode(d->variant, c, sX, sZ, sbits, B, p, maxIter, stop, eX, eZ, flags, rec, iters, q, hp, perm,
-                       d->sector_split, split ? d->merge.data() : nullptr, zeroed, st, rec_stride);
+                       d->sector_split, need_merge ? d->merge.data() : nullptr, zeroed, st, rec_stride);
     if (rc) return rc;
     return ws_release(d, st);
 }

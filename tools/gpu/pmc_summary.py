@@ -2,7 +2,8 @@
 the --pmc passes of `bench.py --no-extras`) into profiles/pmc_<code>.json, which bench.py
 reads for its VALU-issue roofline and `traffic`.
 
-For the BP decode kernel (Kernel_Name contains bp_decode_kernel), per launch:
+For the BP decode kernels (Kernel_Name contains bp_decode_kernel), per decode step (one launch,
+or the X and Z launches of the sector-launch shape, summed):
   * HBM bytes = 2 x FETCH_SIZE + WRITE_SIZE (both reported in KiB), following
     MI355X_MICROARCH.md 'HBM [CDNA4]': on gfx950 FETCH_SIZE counts half the bytes of a
     coalesced streaming read, WRITE_SIZE counts the bytes;
@@ -35,30 +36,42 @@ def counter_rows(d):
 
 
 def per_dispatch(d, kernel=KERNEL):
-    """{counter: [value per dispatch]} and the kernel's metadata, decode kernel only."""
-    vals, meta = {}, {}
-    per = {}
+    """{counter: {kernel name: [value per dispatch]}} and each decode kernel's metadata.  A decode step
+    may be several launches (the sector launches: an X kernel, then a Z kernel), so values are kept
+    per kernel name and a step is the sum over the names of their per-dispatch averages."""
+    per, names, meta = {}, {}, {}
     for row in counter_rows(d):
-        if kernel not in row.get("Kernel_Name", ""):
+        name = row.get("Kernel_Name", "")
+        if kernel not in name:
             continue
         key = (row["Dispatch_Id"], row["Counter_Name"])
         per[key] = per.get(key, 0.0) + float(row["Counter_Value"])
-        meta = {"kernel": row["Kernel_Name"], "vgpr": int(row["VGPR_Count"]), "sgpr": int(row["SGPR_Count"]),
-                "scratch_bytes_per_lane": int(row["Scratch_Size"]), "lds_bytes": int(row["LDS_Block_Size"]),
-                "workgroup": int(row["Workgroup_Size"])}
-    for (_, name), v in per.items():
-        vals.setdefault(name, []).append(v)
+        names[row["Dispatch_Id"]] = name
+        meta[name] = {"vgpr": int(row["VGPR_Count"]), "sgpr": int(row["SGPR_Count"]),
+                      "scratch_bytes_per_lane": int(row["Scratch_Size"]), "lds_bytes": int(row["LDS_Block_Size"]),
+                      "workgroup": int(row["Workgroup_Size"])}
+    vals = {}
+    for (disp, counter), v in per.items():
+        vals.setdefault(counter, {}).setdefault(names[disp], []).append(v)
     return vals, meta
 
 
+def per_step(vals):
+    """{counter: value per decode step}: per kernel name the average over its dispatches, summed."""
+    return {c: sum(sum(v) / len(v) for v in by_name.values()) for c, by_name in vals.items()}
+
+
 def trace_duration_ns(d, kernel=KERNEL):
-    durs = []
+    """Decode time per step: per kernel name the average duration, summed; and the dispatch count."""
+    durs = {}
     for f in glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True):
         with open(f) as fh:
             for row in csv.DictReader(fh):
                 if kernel in row.get("Kernel_Name", ""):
-                    durs.append(int(row["End_Timestamp"]) - int(row["Start_Timestamp"]))
-    return durs
+                    durs.setdefault(row["Kernel_Name"], []).append(int(row["End_Timestamp"]) - int(row["Start_Timestamp"]))
+    if not durs:
+        return None, 0
+    return sum(sum(v) / len(v) for v in durs.values()), sum(len(v) for v in durs.values())
 
 
 def main():
@@ -77,18 +90,23 @@ def main():
         if os.path.isdir(sub):
             v, m = per_dispatch(sub)
             vals.update(v)
-            meta = meta or m
+            meta.update(m)
     if "SQ_INSTS_VALU" not in vals:
         raise SystemExit("no SQ_INSTS_VALU rows for the decode kernel under %s" % a.dir)
-    avg = {k: sum(v) / len(v) for k, v in vals.items()}
-    durs = trace_duration_ns(os.path.join(a.dir, "trace"))
-    dur_ns = sum(durs) / len(durs) if durs else None
+    avg = per_step(vals)
+    dur_ns, ndisp = trace_duration_ns(os.path.join(a.dir, "trace"))
+    kernels = sorted(meta)
     out = {"code": a.code, "batch": batch, "iters": b["config"]["bp_iters"], "stop": b["config"]["stop"],
            "p": b["config"]["p"], "output": b["config"].get("output"), "hard_paths": b["config"].get("hard_paths", 1),
            "input": b["config"].get("input", "bytes"),
-           **meta,
-           "dispatches": {k: len(v) for k, v in vals.items()},
-           "kernel_trace_avg_ns": dur_ns, "kernel_trace_dispatches": len(durs)}
+           "kernel": " + ".join(kernels), "launches_per_step": len(kernels),
+           "vgpr": max(m["vgpr"] for m in meta.values()), "sgpr": max(m["sgpr"] for m in meta.values()),
+           "scratch_bytes_per_lane": max(m["scratch_bytes_per_lane"] for m in meta.values()),
+           "lds_bytes": max(m["lds_bytes"] for m in meta.values()), "workgroup": meta[kernels[0]]["workgroup"],
+           "kernels": meta,
+           "dispatches": {k: sum(len(x) for x in v.values()) for k, v in vals.items()},
+           "kernel_trace_avg_ns": dur_ns, "kernel_trace_dispatches": ndisp,
+           "timing_basis": "per step: each decode kernel's average over its dispatches, summed over the kernels"}
     per_launch = {k: round(v) for k, v in avg.items()}
     out["per_launch"] = per_launch
     # the library the counters were collected on: bench.py uses this profile only for that binary

@@ -1665,8 +1665,11 @@ struct TuneP61MinReg : TuneP61 {};
 using ShiftsP61 = GeneratedShifts<4, 5, 10, 61, 9, 49, TuneP61::kRelabel, TuneP61::kMaskSelect>;
 // P7: three columns per division guard (col_group): 0.075 vs 0.077 ms at configs[1] (65 536 @ 20), even
 // at 2^20 (profiles/r03/cmp_p7_65536_colgroups.txt, cmp_p7_2e20.txt)
+// P7 at 7 waves per SIMD (72 VGPRs): its fixed / reference kernels are spill-free there (8: 2-10 B of
+// scratch) at the same speed (configs[1] 0.071 vs 0.071 ms, 2^20 0.621 vs 0.618 ms;
+// profiles/r04/cmp_p7_waves.txt)
 #ifndef QEC_P7_MINW
-#define QEC_P7_MINW 8
+#define QEC_P7_MINW 7
 #endif
 #ifndef QEC_P7_MWX
 #define QEC_P7_MWX 0
@@ -1674,7 +1677,12 @@ using ShiftsP61 = GeneratedShifts<4, 5, 10, 61, 9, 49, TuneP61::kRelabel, TuneP6
 #ifndef QEC_P7_MWZ
 #define QEC_P7_MWZ 0
 #endif
-using TuneP7 = Tune<QEC_P7_MINW, true, false, true, true, true, false, 2, 1, 7, 3, false, QEC_P7_MWX, QEC_P7_MWZ>;
+// P7 syndrome-stop kernels at 7 waves (4 B of scratch): 6 waves are spill-free but 3-4 % slower
+// (p = 0.05 at 2^20 1.150 vs 1.111 ms; profiles/r04/cmp_p7_syndrome_waves.txt)
+#ifndef QEC_P7_SYNW
+#define QEC_P7_SYNW 7
+#endif
+using TuneP7 = Tune<QEC_P7_MINW, true, false, true, true, true, false, 2, 1, QEC_P7_SYNW, 3, false, QEC_P7_MWX, QEC_P7_MWZ>;
 struct TuneP7MinReg : TuneP7 {};
 using ShiftsP7 = GeneratedShifts<3, 3, 6, 7, 2, 3, TuneP7::kRelabel, TuneP7::kMaskSelect>;
 #ifndef QEC_P61_MINREG

@@ -46,10 +46,12 @@ bool mc_fused_supported(const Code& c, int rec_stride);
 int launch_mc_fused(const Code& c, uint64_t seed, uint64_t start, long long B, float p, const uint32_t pats[4],
                     uint32_t* sX, uint32_t* sZ, uint8_t* rec, int rec_stride, int32_t* iters, uint32_t* merge,
                     int32_t* listX, int32_t* listZ, int32_t* listS, uint32_t* counts, const uint64_t* imp_cols,
-                    unsigned long long* counters, unsigned long long* partials, bool survivors, hipStream_t st);
+                    unsigned long long* counters, unsigned long long* partials, int stage, hipStream_t st);
 long long mc_fused_parts(long long B);
 int mc_fused_count_words();
 int mc_fused_count_stride();
+// u64 words after the counters that hold the fused pipeline's list lengths
+inline int mc_count_u64() { return (mc_fused_count_words() + 3) / 4 * 2; }  // whole 16-byte lines
 int launch_statistics_packed(const Code& c, const uint64_t* imp_cols, const uint8_t* errp, int estride, const uint8_t* rec,
                              const int32_t* iters, long long B, unsigned long long* counters, hipStream_t st,
                              int rec_stride = 0);
@@ -391,7 +393,8 @@ qec_decoder* qec_decoder_create_engine(const qec_code* h, int device, size_t max
             hip_throw(hipMemcpy(d->imp_cols.data(), d->code->imp_cols.data(), d->code->imp_cols.size() * sizeof(uint64_t),
                                 hipMemcpyHostToDevice), "I-P upload");
         }
-        d->mcount.reserve(QEC_MC_NCOUNTERS_ALL);
+        // the counters, then the fused pipeline's list lengths: one memset zeroes both per call
+        d->mcount.reserve(QEC_MC_NCOUNTERS_ALL + mc_count_u64());
         if (d->variant) {
             d->gbar.reserve(2);
             hip_throw(hipMemset(d->gbar.data(), 0, 2 * sizeof(uint32_t)), "grid-barrier words");
@@ -824,7 +827,7 @@ int mc_reserve(qec_decoder* d, size_t B, int W)
 // errors (source filled in h by the caller) -> syndromes + packed errors -> packed decode ->
 // counters, all enqueued on the part's stream
 int mc_batch(qec_decoder* d, McArgsHost h, int src, float p, int maxIter, int stop, bool want_iters,
-             hipEvent_t ev0, hipEvent_t ev1)
+             hipEvent_t ev0, hipEvent_t ev1, bool counts_zeroed = false)
 {
     hipStream_t st = d->stream;
     const Code& c = *d->code;
@@ -848,30 +851,28 @@ int mc_batch(qec_decoder* d, McArgsHost h, int src, float p, int maxIter, int st
         int rc = ws_acquire(d, st);
         if (rc) return rc;
         if ((rc = ws_reserve(d->merge, (size_t)B, st, "monte carlo")) ||
-            (rc = ws_reserve(d->tlist, 3 * (size_t)B + mc_fused_count_words(), st, "monte carlo")) ||
+            (rc = ws_reserve(d->tlist, 3 * (size_t)B, st, "monte carlo")) ||
             (rc = ws_reserve(d->mpart, (size_t)mc_fused_parts(B) * QEC_MC_NCOUNTERS_ALL, st, "monte carlo")))
             return rc;
         int32_t* lX = d->tlist.data();
         int32_t* lZ = lX + B;
         int32_t* lS = lZ + B;
-        uint32_t* cnt = reinterpret_cast<uint32_t*>(lS + B);
+        uint32_t* cnt = reinterpret_cast<uint32_t*>(d->mcount.data() + QEC_MC_NCOUNTERS_ALL);  // list lengths
         uint32_t* sXp = reinterpret_cast<uint32_t*>(d->msX.data());
         uint32_t* sZp = reinterpret_cast<uint32_t*>(d->msZ.data());
-        QEC_HIP_CHECK(hipMemsetAsync(cnt, 0, mc_fused_count_words() * sizeof(uint32_t), st));
+        if (!counts_zeroed) QEC_HIP_CHECK(hipMemsetAsync(cnt, 0, mc_count_u64() * sizeof(unsigned long long), st));
         if (ev0) QEC_HIP_CHECK(hipEventRecord(ev0, st));
-        for (int pass = 0; pass < 2; ++pass) {
-            if (pass == 1) {
-                rc = launch_decode_list(d->variant, c, d->msX.data(), d->msZ.data(), B, p, maxIter, hard_path_bits(d),
-                                        d->mrec.data(), d->mit.data(), d->merge.data(), lX, lZ, cnt, st, rstride, true,
-                                        mc_fused_count_stride());
-                if (rc) return rc;
-                if (ev1) QEC_HIP_CHECK(hipEventRecord(ev1, st));
-            }
-            rc = launch_mc_fused(c, h.seed, h.start, B, h.p, pats, sXp, sZp, d->mrec.data(), rstride, d->mit.data(),
-                                 d->merge.data(), lX, lZ, lS, cnt, d->imp_cols.data(), d->mcount.data(), d->mpart.data(),
-                                 pass == 1, st);
-            if (rc) return rc;
-        }
+        auto fused = [&](int stage) {
+            return launch_mc_fused(c, h.seed, h.start, B, h.p, pats, sXp, sZp, d->mrec.data(), rstride, d->mit.data(),
+                                   d->merge.data(), lX, lZ, lS, cnt, d->imp_cols.data(), d->mcount.data(), d->mpart.data(),
+                                   stage, st);
+        };
+        if ((rc = fused(MC_FUSED_SAMPLE))) return rc;
+        rc = launch_decode_list(d->variant, c, d->msX.data(), d->msZ.data(), B, p, maxIter, hard_path_bits(d), d->mrec.data(),
+                                d->mit.data(), d->merge.data(), lX, lZ, cnt, st, rstride, true, mc_fused_count_stride());
+        if (rc) return rc;
+        if (ev1) QEC_HIP_CHECK(hipEventRecord(ev1, st));
+        if ((rc = fused(MC_FUSED_SURVIVORS))) return rc;
         return ws_release(d, st);
     }
     if (bits) {
@@ -914,7 +915,8 @@ int monte_carlo_part(qec_decoder* d, uint64_t seed, uint64_t start, uint64_t cou
     hipStream_t st = d->stream;
     int rc = mc_reserve(d, (size_t)std::min<uint64_t>(batch, std::max<uint64_t>(count, 1)), 0);
     if (rc) return rc;
-    QEC_HIP_CHECK(hipMemsetAsync(d->mcount.data(), 0, QEC_MC_NCOUNTERS_ALL * sizeof(unsigned long long), st));
+    // the counters and the fused pipeline's list lengths (zeroed again before every later batch)
+    QEC_HIP_CHECK(hipMemsetAsync(d->mcount.data(), 0, (QEC_MC_NCOUNTERS_ALL + mc_count_u64()) * sizeof(unsigned long long), st));
     // decode-kernel time from a ring of event pairs: the host waits only on a pair it reuses,
     // kRing batches behind the launches (no per-batch synchronisation)
     constexpr size_t kRing = 32;
@@ -935,7 +937,7 @@ int monte_carlo_part(qec_decoder* d, uint64_t seed, uint64_t start, uint64_t cou
         McArgsHost h;
         h.seed = seed; h.start = start + base; h.p = p;
         h.B = (long long)std::min<uint64_t>(batch, count - base);
-        rc = mc_batch(d, h, MC_SRC_PHILOX, p, maxIter, stop, true, ev.ev[2 * slot], ev.ev[2 * slot + 1]);
+        rc = mc_batch(d, h, MC_SRC_PHILOX, p, maxIter, stop, true, ev.ev[2 * slot], ev.ev[2 * slot + 1], k == 0);
         if (rc) return rc;
     }
     for (uint64_t j = k > kRing ? k - kRing : 0; j < k; ++j)

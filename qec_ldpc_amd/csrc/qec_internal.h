@@ -65,6 +65,8 @@ struct Mt19937 {
 // mc_errors_syndrome_kernel, or mc_gap_kernel for PHILOX): error source (MC_SRC_*), syndromes out,
 // packed errors out.
 enum { MC_SRC_PHILOX = 0, MC_SRC_DRAWS = 1, MC_SRC_BYTES = 2 };
+// the fused low-p Monte-Carlo pipeline's stages (triage.hip, launch_mc_fused)
+enum { MC_FUSED_SAMPLE = 0, MC_FUSED_SURVIVORS = 1 };
 struct McArgsHost {
     const Code* code = nullptr;
     uint64_t seed = 0, start = 0;

@@ -130,21 +130,35 @@ enum { C_WITHX, C_WITHZ, C_SYNX, C_SYNZ, C_LOGICAL, C_CORRECTED, C_CONVX, C_CONV
 // [8 nb, 16 nb)), else qubit layout (bit q = qubit q of [x | z]).
 constexpr int kMaxWords = 64;  // 2n <= 4096 qubits
 
+// The residual's words are read once (lane k: word k, nw <= 64) and broadcast with readlane, and the
+// columns are fetched four at a time, so a sample costs one LDS round trip and about popcount / 4
+// global ones instead of one per word and one per set bit.
 template <bool REC>
 __device__ __forceinline__ bool logical_from_columns(const unsigned long long* res, int nw, int n, int nb,
                                                      const uint64_t* __restrict__ cols, int cw, int lane)
 {
+    const uint64_t mine = lane < nw ? res[lane] : 0ull;
+    const uint32_t lo = (uint32_t)mine, hi = (uint32_t)(mine >> 32);
+    const bool col_lane = lane < cw;
     uint64_t acc = 0;
     for (int w = 0; w < nw; ++w) {
-        const uint64_t v = res[w];
-        uint64_t bits = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32) |
-                        __builtin_amdgcn_readfirstlane((uint32_t)v);  // uniform: scalar loop below
-        while (bits) {
-            const int j = __builtin_ctzll(bits);
-            bits &= bits - 1;
-            int q = 64 * w + j;
-            if (REC) q = q < 8 * nb ? q : n + (q - 8 * nb);
-            if (lane < cw) acc ^= cols[(size_t)q * cw + lane];
+        uint64_t bits = ((uint64_t)__builtin_amdgcn_readlane(hi, w) << 32) | __builtin_amdgcn_readlane(lo, w);
+        while (bits) {  // uniform
+            int q[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                q[u] = -1;
+                if (bits) {
+                    const int j = __builtin_ctzll(bits);
+                    bits &= bits - 1;
+                    const int qq = 64 * w + j;
+                    q[u] = REC ? (qq < 8 * nb ? qq : n + (qq - 8 * nb)) : qq;
+                }
+            }
+            uint64_t c[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) c[u] = (q[u] >= 0 && col_lane) ? cols[(size_t)q[u] * cw + lane] : 0ull;
+            acc ^= (c[0] ^ c[1]) ^ (c[2] ^ c[3]);
         }
     }
     return __any(acc != 0);

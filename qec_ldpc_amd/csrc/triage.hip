@@ -20,8 +20,8 @@
 // sectors of a syndrome meet in its merge word as in the sector-split launches (done bit + flags).
 //
 // The fused Monte-Carlo form (mc_fused_kernel, qec_monte_carlo at low p): sampler -> syndrome bits in
-// LDS -> this triage -> residual against the sample's hits -> I-P check -> counters, in one kernel; only
-// the samples with a sector that goes on (about 1 % of P61 samples at p = 0.002) reach HBM, for the
+// LDS -> this triage -> decision against the sample's hits -> counters, in one kernel; only the
+// samples that are not finished there (about 1 % of P61 samples at p = 0.002) reach HBM, for the
 // list-mode decode and the survivor statistics (mc_survivor_kernel, which walks the sample again).
 #include <hip/hip_runtime.h>
 
@@ -373,23 +373,34 @@ __global__ __launch_bounds__(64 * kTriageWaves) void triage_kernel(const TriageA
 //      syndrome bit rows in LDS (as mc_gap_kernel) and is kept in the lane's hit list (qubit << 2 | type,
 //      up to kHitCap of them);
 //   2. the iteration-0 triage of both sectors on those rows (triage_both);
-//   3. a sample whose two sectors stop there and whose hits fit the list is finished here: its decision
-//      equals its error iff every hit qubit is decided in its sector(s) and nothing else is (counts of
-//      set bits), else the residual goes through the I-P columns (logical_from_columns), and the
-//      CodeStatistics counters (DecoderCPU.h:464-521) are counted with iterations 1 + 1;
-//   4. any other sample (a sector goes on, or more hits than the list holds) is a survivor: its
-//      syndrome rows, its record with the triage's decisions, its iteration counts and merge word are
-//      written as the triage kernel writes them, it is appended to listX / listZ for the sectors that
-//      go on and to listS, and mc_survivor_kernel counts it after the list-mode decode.
+//   3. a sample whose two sectors stop there, whose hits fit the list and whose decision equals its
+//      error (every hit qubit decided in its sector(s) and nothing else: counts of set bits) is
+//      finished here, corrected with iterations 1 + 1 (DecoderCPU.h:464-521); the triage runs sector by
+//      sector, so one sector's decisions are live at a time (registers: occupancy);
+//   4. any other sample is a survivor: it gets what the triage kernel writes for a syndrome
+//      (syndrome rows, record with the iteration-0 decisions, iteration counts, merge word; listX /
+//      listZ for the sectors that go on) and is appended to listS; the list-mode decode runs, and
+//      mc_survivor_kernel counts the survivors (I-P check included: a stopped survivor whose decision
+//      differs from its error is decided there).
 // withX / withZ (errors present) are counted here for every sample.
-// 16-wave workgroups: the workgroup-level atomics (list appends) are few, and the counters go to
-// per-workgroup partial sums (mc_reduce_kernel) -- same-address atomics from every workgroup
-// serialise at L2 (one per workgroup and counter at 4-wave workgroups: ~37 k per 2^20 samples)
+// 4-wave workgroups: six fit a CU's LDS (23 words per lane for P61: rows and up to six hits) and the
+// registers are held to six waves per SIMD (measured against 8, 12 and 16-wave workgroups and ten or
+// sixteen hits: +2-9 %; a sample with more hits is a survivor); the list appends take one atomic
+// per workgroup and list, and the counters go to per-workgroup partial sums that
+// mc_survivor_kernel's first workgroups add up (same-address atomics serialise at L2)
 #ifndef QEC_FUSED_WAVES
-#define QEC_FUSED_WAVES 16
+#define QEC_FUSED_WAVES 4
+#endif
+#ifndef QEC_FUSED_HITS
+#define QEC_FUSED_HITS 6
+#endif
+#ifndef QEC_FUSED_MINW
+#define QEC_FUSED_MINW 6
 #endif
 constexpr int kFusedWaves = QEC_FUSED_WAVES;
-constexpr int kHitCap = 16;  // hits a lane keeps (P61 at p = 0.01: 6.1 on average)
+constexpr int kFusedMinWaves = QEC_FUSED_MINW;  // waves per SIMD the registers must allow
+constexpr int kHitCap = QEC_FUSED_HITS;  // hits a lane keeps (P61: 1.2 on average at p = 0.002, 3.1 at 0.005)
+constexpr uint32_t kXClean = 0x400u;  // merge word: the X sector stopped with the sample's X errors
 constexpr int kCountStride = 32;  // words between the three list lengths (separate L2 lines)
 
 struct FusedArgs {
@@ -434,46 +445,6 @@ __device__ __forceinline__ void store_partials(const unsigned long long (&c)[C_N
     }
 }
 
-// one workgroup: the partial sums of mc_fused_kernel added to the counters (C_N + 2 atomics)
-__global__ __launch_bounds__(256) void mc_reduce_kernel(const unsigned long long* __restrict__ partials, int nparts,
-                                                        unsigned long long* __restrict__ counters)
-{
-    __shared__ unsigned long long acc[256 / 64][C_N + 2];
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    unsigned long long v[C_N + 2] = {};
-    for (int w = threadIdx.x; w < nparts; w += blockDim.x)
-#pragma unroll
-        for (int k = 0; k < C_N + 2; ++k) v[k] += partials[(size_t)w * (C_N + 2) + k];
-#pragma unroll
-    for (int k = 0; k < C_N + 2; ++k)
-#pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) v[k] += __shfl_xor(v[k], o);
-    if (lane == 0)
-#pragma unroll
-        for (int k = 0; k < C_N + 2; ++k) acc[wv][k] = v[k];
-    __syncthreads();
-    if (threadIdx.x < C_N + 2) {
-        unsigned long long t = 0;
-        for (int w = 0; w < 256 / 64; ++w) t += acc[w][threadIdx.x];
-        if (t) atomicAdd(&counters[threadIdx.x], t);
-    }
-}
-
-// Decision bits of this lane's sample in the record layout (x bits at [0, 8 nb), z at [8 nb, 16 nb)), as
-// u32 words [0, 2 NW) with the flags byte left 0, XOR its hits: the residual the I-P check takes.
-template <int L, int P, int NW>
-__device__ __forceinline__ void residual_words(uint32_t* __restrict__ out, const uint64_t (&hdX)[L], const uint64_t (&hdZ)[L],
-                                               const uint16_t* __restrict__ hits, int nh)
-{
-    constexpr int nb = (L * P + 7) / 8;
-    stage_record_dw<L, P>(out, 2 * NW, hdX, hdZ, 0u);
-    for (int h = 0; h < nh; ++h) {
-        const int v = hits[h] >> 2, t = hits[h] & 3;
-        if (t != 2) out[v >> 5] ^= 1u << (v & 31);
-        if (t != 0) out[(8 * nb + v) >> 5] ^= 1u << ((8 * nb + v) & 31);
-    }
-}
-
 // the wave's counters (ballot popcounts, iteration sums) added to the global ones once per workgroup
 template <int NWAVES>
 __device__ __forceinline__ void flush_counters(const unsigned long long (&c)[C_N + 2], unsigned long long (*part)[C_N + 2],
@@ -494,19 +465,95 @@ __device__ __forceinline__ void flush_counters(const unsigned long long (&c)[C_N
     }
 }
 
+// One sector of this lane's sample, from its syndrome row in LDS: the iteration-0 triage (ok: the
+// decision satisfies the syndrome), and whether that decision is exactly the sample's errors in this
+// sector -- each hit qubit of the sector (type != Z for X, != X for Z) decided and no other bit set (the
+// walk hits a qubit at most once).  Only one sector's decisions are live at a time.
+// on_hd(hd, ok, cvb, match) runs while the decisions are live (the survivors' record words).
+template <int R, int L, int P, class EXP, int SEC, class F>
+__device__ __forceinline__ bool fused_sector(const TriageMasks& m, const uint32_t* __restrict__ syn,
+                                             const uint16_t* __restrict__ hits, int nh, bool check, bool& cvb,
+                                             bool& match, F&& on_hd)
+{
+    constexpr int kW = row_words<R, P>();
+    uint32_t w[kW + 2];
+#pragma unroll
+    for (int k = 0; k < kW; ++k) w[k] = syn[k];
+    w[kW] = w[kW + 1] = 0u;
+    uint64_t hd[L];
+    bool ok;
+    if (R >= 4 && (SEC ? m.symZ : m.symX))
+        ok = triage_sector<R, L, P, EXP, SEC, (R >= 4)>(w, SEC ? m.hdpatZ : m.hdpatX, SEC ? m.cvpatZ : m.cvpatX,
+                                                        SEC ? m.hdcntZ : m.hdcntX, SEC ? m.cvcntZ : m.cvcntX, hd, cvb);
+    else
+        ok = triage_sector<R, L, P, EXP, SEC, false>(w, SEC ? m.hdpatZ : m.hdpatX, SEC ? m.cvpatZ : m.cvpatX, 0u, 0u,
+                                                     hd, cvb);
+    match = false;
+    if (check && ok) {
+        int cnt = 0, hs = 0;
+        bool mt = true;
+#pragma unroll
+        for (int l = 0; l < L; ++l) cnt += __popcll(hd[l]);
+        for (int h = 0; h < nh; ++h) {
+            const int v = hits[h] >> 2, t = hits[h] & 3;
+            if (t == (SEC ? 0 : 2)) continue;  // X-only hit in Z, Z-only hit in X
+            const int l = v / P, j = v - l * P;
+            uint64_t x = 0;
+#pragma unroll
+            for (int q = 0; q < L; ++q) x = q == l ? hd[q] : x;  // select, not a dynamic register index
+            mt &= ((x >> j) & 1ull) != 0ull;
+            ++hs;
+        }
+        match = mt && cnt == hs;
+    }
+    on_hd(hd, ok, cvb, match);
+    return ok;
+}
+
+// One sector's record dwords (stage_record_dw's layout: sector s at bits [8 nb s, 8 nb s + n), flags
+// byte at bit 16 nb) into the record row, ndw dwords: the X sector keeps the dword it shares with the
+// Z sector in carry, the Z sector ORs carry in and writes the flags and the row's padding.
+template <int L, int P, int SEC>
+__device__ __forceinline__ void stage_sector_dw(uint32_t* __restrict__ row, int ndw, const uint64_t (&hd)[L], uint32_t flags,
+                                                uint32_t& carry)
+{
+    constexpr int n = L * P, nb = (n + 7) / 8, s0 = 8 * nb * SEC;
+    constexpr int d0 = s0 / 32, d1 = (s0 + n - 1) / 32;
+    constexpr int z0 = 8 * nb / 32;                 // the Z sector's first dword
+    constexpr bool shared = (8 * nb) % 32 != 0;     // which also holds the X sector's last bits
+    constexpr int fb = 16 * nb;
+#pragma unroll
+    for (int d = d0; d <= d1; ++d) {
+        uint32_t w = 0;
+#pragma unroll
+        for (int l = 0; l < L; ++l) {
+            const int a0 = 32 * d - (s0 + P * l);  // block bit at this dword's bit 0
+            if (a0 >= P || a0 <= -32) continue;
+            w |= a0 >= 0 ? (uint32_t)(hd[l] >> a0) : (uint32_t)(hd[l] << (-a0));
+        }
+        if (SEC == 0 && shared && d == z0) {
+            carry = w;
+            continue;
+        }
+        if (SEC == 1 && d == d0) w |= carry;
+        if (SEC == 1 && fb >= 32 * d && fb < 32 * d + 32) w |= flags << (fb - 32 * d);
+        row[d] = w;
+    }
+    if (SEC == 1)
+        for (int d = d1 + 1; d < ndw; ++d) row[d] = (fb >= 32 * d && fb < 32 * d + 32) ? flags << (fb - 32 * d) : 0u;
+}
+
 template <int J, int K, int L, int P, int S, int T_>
-__global__ __launch_bounds__(64 * kFusedWaves) void mc_fused_kernel(const FusedArgs a)
+__global__ __launch_bounds__(64 * kFusedWaves, kFusedMinWaves) void mc_fused_kernel(const FusedArgs a)
 {
     using EXP = QcExponents<J, K, L, P, S, T_>;
     constexpr EXP tab = EXP::make();
-    constexpr int n = L * P, nb = (n + 7) / 8;
+    constexpr int n = L * P;
     constexpr int kWX = row_words<J, P>(), kWZ = row_words<K, P>();
-    constexpr int RS = (kWX + kWZ + kHitCap / 2) | 1;  // lane region (odd: the lanes' words in distinct banks)
-    constexpr int NW = (2 * nb + 7) / 8;                // 64-bit residual words (record layout)
+    constexpr int RS = (kWX + kWZ + (kHitCap + 1) / 2) | 1;  // lane region (odd: the lanes' words in distinct banks)
     __shared__ uint32_t T[n + 1];
     __shared__ int E[(J + K) * L];
     __shared__ uint32_t region[64 * kFusedWaves * RS];
-    __shared__ unsigned long long sres[kFusedWaves][NW];
     __shared__ unsigned long long part[kFusedWaves][C_N + 2];
     __shared__ uint32_t wcnt[kFusedWaves][3], wgbase[3];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -549,66 +596,45 @@ __global__ __launch_bounds__(64 * kFusedWaves) void mc_fused_kernel(const FusedA
                 }
         });
     }
-    uint32_t wX[kWX + 2], wZ[kWZ + 2];
-#pragma unroll
-    for (int k = 0; k < kWX; ++k) wX[k] = synX[k];
-#pragma unroll
-    for (int k = 0; k < kWZ; ++k) wZ[k] = synZ[k];
-    wX[kWX] = wX[kWX + 1] = wZ[kWZ] = wZ[kWZ + 1] = 0u;
-    uint64_t hdX[L], hdZ[L];
-    bool cvbX = false, cvbZ = false, okX, okZ;
-    triage_both<J, K, L, P, EXP>(a.m, wX, wZ, hdX, hdZ, cvbX, cvbZ, okX, okZ);
-    const uint32_t fX = cvbX ? QEC_CONVERGENCE_FAIL_X : 0u, fZ = cvbZ ? QEC_CONVERGENCE_FAIL_Z : 0u;
-    const bool done = valid && okX && okZ && nh <= kHitCap;
+    const bool fits = valid && nh <= kHitCap;
+    // survivors get what the triage kernel writes, sector by sector while its decisions are live
+    // (one sector's decisions in registers at a time): the X sector's record words when X is not
+    // clean, the Z sector's and the flags for every survivor.  A clean X sector (stopped, decision = errors) of a
+    // survivor keeps no record words: merge bit kXClean tells mc_survivor_kernel its residual is 0.
+    uint32_t* __restrict__ recrow = reinterpret_cast<uint32_t*>(a.rec + b * a.recB);
+    uint32_t carry = 0u, fX = 0u;
+    bool cvbX = false, cvbZ = false, mX, mZ;
+    const bool okX = fused_sector<J, L, P, EXP, 0>(a.m, synX, hits, nh, fits, cvbX, mX,
+                                                   [&](const uint64_t (&hd)[L], bool ok, bool cvb, bool mt) {
+                                                       fX = cvb ? QEC_CONVERGENCE_FAIL_X : 0u;
+                                                       if (valid && !(fits && ok && mt))
+                                                           stage_sector_dw<L, P, 0>(recrow, a.recB >> 2, hd, 0u, carry);
+                                                   });
+    const bool xclean = fits && okX && mX;
+    uint32_t fZ = 0u;
+    const bool okZ = fused_sector<K, L, P, EXP, 1>(a.m, synZ, hits, nh, xclean, cvbZ, mZ,
+                                                   [&](const uint64_t (&hd)[L], bool ok, bool cvb, bool mt) {
+                                                       fZ = cvb ? QEC_CONVERGENCE_FAIL_Z : 0u;
+                                                       if (valid && !(xclean && ok && mt))
+                                                           stage_sector_dw<L, P, 1>(recrow, a.recB >> 2, hd, fX | fZ, carry);
+                                                   });
+    // finished: both sectors stop at iteration 0 with the decision equal to the error (corrected)
+    const bool done = xclean && okZ && mZ;
     const bool surv = valid && !done;
-    // a finished sample's decision equals its error iff each hit qubit is decided in its sector(s) and
-    // the decisions hold no other bit (the walk hits a qubit at most once)
-    bool match = true;
-    if (done) {
-        int cx = 0, cz = 0, hx = 0, hz = 0;
+    if (surv) {  // its syndrome rows, for the list-mode decode
 #pragma unroll
-        for (int l = 0; l < L; ++l) { cx += __popcll(hdX[l]); cz += __popcll(hdZ[l]); }
-        for (int h = 0; h < nh; ++h) {
-            const int v = hits[h] >> 2, t = hits[h] & 3;
-            const int l = v / P, j = v - l * P;
-            uint64_t x = 0, z = 0;
+        for (int k = 0; k < kWX; ++k) a.sX[b * kWX + k] = synX[k];
 #pragma unroll
-            for (int q = 0; q < L; ++q) {  // select, not a dynamic register index
-                x = q == l ? hdX[q] : x;
-                z = q == l ? hdZ[q] : z;
-            }
-            if (t != 2) { match &= ((x >> j) & 1ull) != 0ull; ++hx; }
-            if (t != 0) { match &= ((z >> j) & 1ull) != 0ull; ++hz; }
-        }
-        match &= cx == hx && cz == hz;
-    }
-    // the rare finished sample whose decision differs from its error: the I-P check, one at a time
-    unsigned long long need = __ballot(done && !match), logical = 0;
-    while (need) {
-        const int sl = __builtin_ctzll(need);
-        need &= need - 1;
-        if (lane == sl) residual_words<L, P, NW>(reinterpret_cast<uint32_t*>(sres[wv]), hdX, hdZ, hits, nh);
-        wave_sync();
-        if (logical_from_columns<true>(sres[wv], NW, n, nb, a.imp_cols, a.imp_cw, lane)) logical |= 1ull << sl;
-        wave_sync();
-    }
-    // survivors: what the triage kernel writes for a syndrome, and the lists
-    if (surv) {
-#pragma unroll
-        for (int k = 0; k < kWX; ++k) a.sX[b * kWX + k] = wX[k];
-#pragma unroll
-        for (int k = 0; k < kWZ; ++k) a.sZ[b * kWZ + k] = wZ[k];
-        stage_record_dw<L, P>(reinterpret_cast<uint32_t*>(a.rec + b * a.recB), a.recB >> 2, hdX, hdZ, fX | fZ);
+        for (int k = 0; k < kWZ; ++k) a.sZ[b * kWZ + k] = synZ[k];
         *reinterpret_cast<int2*>(a.iters + 2 * b) = make_int2(1, 1);  // list sectors rewrite theirs
-        a.merge[b] = (okX ? 0x100u | fX : 0u) | (okZ ? 0x200u | fZ : 0u);
+        a.merge[b] = (okX ? 0x100u | fX : 0u) | (okZ ? 0x200u | fZ : 0u) | (xclean ? kXClean : 0u);
     }
-    const unsigned long long gx = __ballot(surv && !okX), gz = __ballot(surv && !okZ), gs = __ballot(surv);
-    const unsigned long long dm = __ballot(done);
+    const unsigned long long gs = __ballot(surv), dm = __ballot(done);
+    const unsigned long long gx = __ballot(surv && !okX), gz = __ballot(surv && !okZ);
     unsigned long long c[C_N + 2] = {};
     c[C_WITHX] = __popcll(__ballot(valid && anyX));
     c[C_WITHZ] = __popcll(__ballot(valid && anyZ));
-    c[C_LOGICAL] = __popcll(dm & logical);
-    c[C_CORRECTED] = __popcll(dm & ~logical);
+    c[C_CORRECTED] = __popcll(dm);
     c[C_CONVX] = __popcll(__ballot(done && cvbX));
     c[C_CONVZ] = __popcll(__ballot(done && cvbZ));
     c[C_N] = c[C_N + 1] = __popcll(dm);  // one iteration per sector
@@ -642,6 +668,42 @@ __global__ __launch_bounds__(64 * kFusedWaves) void mc_fused_kernel(const FusedA
 // the residual is nonzero, convergence fails, both iteration counts).  withX / withZ were counted by
 // mc_fused_kernel.
 constexpr int kSurvWaves = 4;
+constexpr int kReduceGroups = 16;  // its first workgroups also add mc_fused_kernel's partial sums
+
+// One lane of an I-P check group (CheckLogicalError, Quantum_LDPC_Code.h:126-142, as
+// logical_from_columns): word k of the XOR of the I-P columns at the set bits of the residual res[0, nw)
+// (u32 words, record layout: x bits at [0, 8 nb), z bits from 8 nb) is nonzero.  Every lane of a group
+// walks the same residual; the columns are fetched four at a time.
+template <int L, int P>
+__device__ __forceinline__ bool logical_group(const uint32_t* __restrict__ res, int nw, bool active,
+                                              const uint64_t* __restrict__ cols, int cw, int k)
+{
+    constexpr int n = L * P, nb = (n + 7) / 8;
+    uint64_t acc = 0;
+    if (active && k < cw) {
+        for (int w = 0; w < nw; ++w) {
+            uint32_t bits = res[w];
+            while (bits) {
+                int q[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    q[u] = -1;
+                    if (bits) {
+                        const int qq = 32 * w + __builtin_ctz(bits);
+                        bits &= bits - 1;
+                        q[u] = qq < 8 * nb ? qq : n + (qq - 8 * nb);
+                    }
+                }
+                uint64_t c[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) c[u] = q[u] >= 0 ? cols[(size_t)q[u] * cw + k] : 0ull;
+                acc ^= (c[0] ^ c[1]) ^ (c[2] ^ c[3]);
+            }
+        }
+    }
+    return acc != 0ull;
+}
+
 
 template <int L, int P>
 __global__ __launch_bounds__(64 * kSurvWaves) void mc_survivor_kernel(const FusedArgs a)
@@ -651,16 +713,32 @@ __global__ __launch_bounds__(64 * kSurvWaves) void mc_survivor_kernel(const Fuse
     constexpr int RS = (2 * NW) | 1;  // lane region in u32 words (odd stride)
     __shared__ uint32_t T[n + 1];
     __shared__ uint32_t region[64 * kSurvWaves * RS];
-    __shared__ unsigned long long sres[kSurvWaves][NW];
     __shared__ unsigned long long part[kSurvWaves][C_N + 2];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    if (blockIdx.x < kReduceGroups) {  // mc_fused_kernel's per-workgroup partial sums into the counters
+        const int R = (int)gridDim.x < kReduceGroups ? (int)gridDim.x : kReduceGroups;
+        unsigned long long v[C_N + 2] = {};
+        for (long long w = blockIdx.x + (long long)R * threadIdx.x; w < a.nparts; w += (long long)R * blockDim.x)
+#pragma unroll
+            for (int q = 0; q < C_N + 2; ++q) v[q] += a.partials[w * (C_N + 2) + q];
+#pragma unroll
+        for (int q = 0; q < C_N + 2; ++q)
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) v[q] += __shfl_xor(v[q], o);
+        flush_counters<kSurvWaves>(v, part, a.counters);
+        __syncthreads();  // part is used again below
+    }
     const long long cnt = a.counts[2 * kCountStride];
     if ((long long)blockIdx.x * blockDim.x >= cnt) return;  // workgroup-uniform: no survivor for this one
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     gap_table(a.gp, n, T);
     __syncthreads();
     uint32_t* __restrict__ mine = region + threadIdx.x * RS;
     unsigned long long c[C_N + 2] = {};
     const long long step = (long long)gridDim.x * blockDim.x;
+    // the I-P checks' lane groups: G = 64 / imp_cw samples per pass, lane k of a group sums word k
+    const int G = a.imp_cw > 0 ? 64 / a.imp_cw : 1;
+    const int g = a.imp_cw > 0 ? lane / a.imp_cw : 0, k = lane - g * a.imp_cw;
+    const unsigned long long gmask = a.imp_cw >= 64 ? ~0ull : (1ull << a.imp_cw) - 1ull;
     for (long long i0 = (long long)blockIdx.x * blockDim.x + wv * 64; i0 < cnt; i0 += step) {
         const long long idx = i0 + lane;
         const bool valid = idx < cnt;
@@ -676,31 +754,42 @@ __global__ __launch_bounds__(64 * kSurvWaves) void mc_survivor_kernel(const Fuse
         const uint32_t* __restrict__ r = reinterpret_cast<const uint32_t*>(a.rec + b * a.recB);
         constexpr int kRW = (2 * nb + 3) / 4;  // record words holding decisions
         static_assert(kRW <= 2 * NW, "the lane region holds the record's words");
+        const uint32_t mw = valid ? a.merge[b] : 0u;
+        const bool xclean = (mw & kXClean) != 0u;  // X residual 0; no X record words
         uint32_t nz = 0;
 #pragma unroll
-        for (int k = 0; k < kRW; ++k) {
-            const uint32_t rv = valid ? r[k] : 0u;
-            const int rem = 2 * nb - 4 * k;  // decision bytes in word k
-            const uint32_t m = rem >= 4 ? ~0u : rem <= 0 ? 0u : (1u << (8 * rem)) - 1u;
-            const uint32_t res = (mine[k] ^ rv) & m;
-            mine[k] = res;
+        for (int d = 0; d < kRW; ++d) {
+            const uint32_t rv = valid ? r[d] : 0u;
+            const int rem = 2 * nb - 4 * d;  // decision bytes in word d
+            const int xb = n - 32 * d;       // X decision bits in word d
+            const uint32_t xm = xb >= 32 ? ~0u : xb <= 0 ? 0u : (1u << xb) - 1u;
+            const uint32_t m = (rem >= 4 ? ~0u : rem <= 0 ? 0u : (1u << (8 * rem)) - 1u) & (xclean ? ~xm : ~0u);
+            const uint32_t res = (mine[d] ^ rv) & m;
+            mine[d] = res;
             nz |= res;
         }
         // the flags: the list-mode decode ORs its sectors' into the merge word, which the fused kernel
         // set to the stopped sectors' (launch_decode_list, merge_only); the record's byte is not merged
-        const uint32_t f = valid ? (a.merge[b] & 0xFFu) : 0u;
+        const uint32_t f = mw & 0xFFu;
         const bool sx = (f & QEC_SYNDROME_FAIL_X) != 0, sz = (f & QEC_SYNDROME_FAIL_Z) != 0;
-        unsigned long long need = __ballot(valid && !(sx || sz) && nz != 0u), logical = 0;
-        while (need) {
-            const int sl = __builtin_ctzll(need);
-            need &= need - 1;
-            if (lane < NW) {
-                const uint32_t* src = region + (wv * 64 + sl) * RS;
-                sres[wv][lane] = (unsigned long long)src[2 * lane] | ((unsigned long long)src[2 * lane + 1] << 32);
+        unsigned long long need = a.imp_cw > 0 ? __ballot(valid && !(sx || sz) && nz != 0u) : 0ull, logical = 0;
+        wave_sync();  // the residuals, read across lanes
+        while (need) {  // G samples per pass: lane group g (imp_cw lanes) takes the pass's g-th sample
+            const unsigned long long pick = need;
+            int s = -1;
+            for (int q = 0; q < G && need; ++q) {
+                const int sl = __builtin_ctzll(need);
+                need &= need - 1;
+                if (q == g) s = sl;
             }
-            wave_sync();
-            if (logical_from_columns<true>(sres[wv], NW, n, nb, a.imp_cols, a.imp_cw, lane)) logical |= 1ull << sl;
-            wave_sync();
+            const unsigned long long nzm = __ballot(logical_group<L, P>(region + (wv * 64 + (s < 0 ? 0 : s)) * RS, kRW, s >= 0,
+                                                                        a.imp_cols, a.imp_cw, k));
+            unsigned long long p2 = pick;
+            for (int q = 0; q < G && p2; ++q) {
+                const int sl = __builtin_ctzll(p2);
+                p2 &= p2 - 1;
+                if ((nzm >> (q * a.imp_cw)) & gmask) logical |= 1ull << sl;
+            }
         }
         const unsigned long long vm = __ballot(valid), bx = __ballot(sx), bz = __ballot(sz);
         const unsigned long long ok = vm & ~(bx | bz);
@@ -777,11 +866,14 @@ static TriageMasks triage_masks(const Code& c, const uint32_t pats[4])
 using FusedFn = void (*)(const FusedArgs);
 
 // the fused kernels of the shipped codes (as triage_fn)
-static bool fused_fns(const Code& c, FusedFn& fused, FusedFn& surv)
+struct FusedFns {
+    FusedFn fused, surv;
+};
+static bool fused_fns(const Code& c, FusedFns& f)
 {
     if (!triage_supported(c)) return false;
-    if (c.P == 61) { fused = mc_fused_kernel<4, 5, 10, 61, 9, 49>; surv = mc_survivor_kernel<10, 61>; }
-    else { fused = mc_fused_kernel<3, 3, 6, 7, 2, 3>; surv = mc_survivor_kernel<6, 7>; }
+    if (c.P == 61) f = {mc_fused_kernel<4, 5, 10, 61, 9, 49>, mc_survivor_kernel<10, 61>};
+    else f = {mc_fused_kernel<3, 3, 6, 7, 2, 3>, mc_survivor_kernel<6, 7>};
     return true;
 }
 
@@ -793,21 +885,25 @@ int mc_fused_count_stride() { return kCountStride; }
 
 bool mc_fused_supported(const Code& c, int rec_stride)
 {
-    FusedFn f, s;
-    return fused_fns(c, f, s) && rec_stride % 4 == 0 && rec_stride >= 2 * ((c.n + 7) / 8) + 1 &&
+    FusedFns f;
+    return fused_fns(c, f) && rec_stride % 4 == 0 && rec_stride >= 2 * ((c.n + 7) / 8) + 1 &&
            c.imp_col_words <= 64 && 2 * c.n < (1 << 14);
 }
 
-// The fused pipeline's first kernel (sample, syndromes, triage, finished samples' statistics) and,
-// after the caller's list-mode decode, the survivors' statistics.  counts[3] must be zeroed first.
+// The fused pipeline's kernels, in stage order on one stream: MC_FUSED_SAMPLE (sample, syndromes,
+// triage, the finished samples' statistics, the survivors' triage outputs and lists), then -- after
+// the caller's list-mode decode -- MC_FUSED_SURVIVORS (their statistics).  counts must be zeroed
+// before the first.
 int launch_mc_fused(const Code& c, uint64_t seed, uint64_t start, long long B, float p, const uint32_t pats[4],
                     uint32_t* sX, uint32_t* sZ, uint8_t* rec, int rec_stride, int32_t* iters, uint32_t* merge,
                     int32_t* listX, int32_t* listZ, int32_t* listS, uint32_t* counts, const uint64_t* imp_cols,
-                    unsigned long long* counters, unsigned long long* partials, bool survivors, hipStream_t st)
+                    unsigned long long* counters, unsigned long long* partials, int stage, hipStream_t st)
 {
-    FusedFn fused = nullptr, surv = nullptr;
-    if (!mc_fused_supported(c, rec_stride) || !fused_fns(c, fused, surv))
+    FusedFns f{};
+    if (!mc_fused_supported(c, rec_stride) || !fused_fns(c, f))
         return fail(QEC_ERR_UNSUPPORTED, "mc fused: no kernel for this code or record layout");
+    if ((reinterpret_cast<uintptr_t>(sX) | reinterpret_cast<uintptr_t>(sZ)) & 7u || reinterpret_cast<uintptr_t>(iters) & 7u)
+        return fail(QEC_ERR_ARG, "mc fused: bit rows and iteration counts must be 8-byte aligned");
     if (B <= 0) return QEC_OK;
     FusedArgs a{};
     a.gp = make_gap(seed, p);
@@ -817,19 +913,17 @@ int launch_mc_fused(const Code& c, uint64_t seed, uint64_t start, long long B, f
     a.listX = listX; a.listZ = listZ; a.listS = listS; a.counts = counts;
     a.imp_cols = imp_cols; a.imp_cw = c.imp_col_words; a.counters = counters;
     a.partials = partials; a.nparts = (int)mc_fused_parts(B);
-    if (!survivors) {
-        hipLaunchKernelGGL(fused, dim3((unsigned)a.nparts), dim3(64 * kFusedWaves), 0, st, a);
-        hipError_t e = hipGetLastError();
-        if (e != hipSuccess) return fail(QEC_ERR_HIP, std::string("mc fused launch: ") + hipGetErrorString(e));
-        hipLaunchKernelGGL(mc_reduce_kernel, dim3(1), dim3(256), 0, st, partials, a.nparts, counters);
+    if (stage == MC_FUSED_SAMPLE) {
+        hipLaunchKernelGGL(f.fused, dim3((unsigned)a.nparts), dim3(64 * kFusedWaves), 0, st, a);
     } else {
+        // the survivor count is on the device: a grid for up to every sample, capped (grid-stride)
         int dev = 0, cus = 256;
         if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
             cus <= 0)
             cus = 256;
         const long long per = 64LL * kSurvWaves;
         const long long blocks = std::min<long long>((B + per - 1) / per, 2LL * cus);
-        hipLaunchKernelGGL(surv, dim3((unsigned)blocks), dim3(64 * kSurvWaves), 0, st, a);
+        hipLaunchKernelGGL(f.surv, dim3((unsigned)blocks), dim3(64 * kSurvWaves), 0, st, a);
     }
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(QEC_ERR_HIP, std::string("mc fused launch: ") + hipGetErrorString(e));

@@ -826,8 +826,10 @@ int mc_reserve(qec_decoder* d, size_t B, int W)
 
 // errors (source filled in h by the caller) -> syndromes + packed errors -> packed decode ->
 // counters, all enqueued on the part's stream
+// zero_counters: the call's first batch (the counters start at 0; one memset with the fused
+// pipeline's list lengths, enqueued after the host-side preparation, right before the first kernel)
 int mc_batch(qec_decoder* d, McArgsHost h, int src, float p, int maxIter, int stop, bool want_iters,
-             hipEvent_t ev0, hipEvent_t ev1, bool counts_zeroed = false)
+             hipEvent_t ev0, hipEvent_t ev1, bool zero_counters = false)
 {
     hipStream_t st = d->stream;
     const Code& c = *d->code;
@@ -860,7 +862,10 @@ int mc_batch(qec_decoder* d, McArgsHost h, int src, float p, int maxIter, int st
         uint32_t* cnt = reinterpret_cast<uint32_t*>(d->mcount.data() + QEC_MC_NCOUNTERS_ALL);  // list lengths
         uint32_t* sXp = reinterpret_cast<uint32_t*>(d->msX.data());
         uint32_t* sZp = reinterpret_cast<uint32_t*>(d->msZ.data());
-        if (!counts_zeroed) QEC_HIP_CHECK(hipMemsetAsync(cnt, 0, mc_count_u64() * sizeof(unsigned long long), st));
+        if (zero_counters)
+            QEC_HIP_CHECK(hipMemsetAsync(d->mcount.data(), 0, (QEC_MC_NCOUNTERS_ALL + mc_count_u64()) * sizeof(unsigned long long), st));
+        else
+            QEC_HIP_CHECK(hipMemsetAsync(cnt, 0, mc_count_u64() * sizeof(unsigned long long), st));
         if (ev0) QEC_HIP_CHECK(hipEventRecord(ev0, st));
         auto fused = [&](int stage) {
             return launch_mc_fused(c, h.seed, h.start, B, h.p, pats, sXp, sZp, d->mrec.data(), rstride, d->mit.data(),
@@ -883,6 +888,7 @@ int mc_batch(qec_decoder* d, McArgsHost h, int src, float p, int maxIter, int st
         h.sX = d->msX.data(); h.sZ = d->msZ.data();
     }
     h.errp = d->merrp.data();
+    if (zero_counters) QEC_HIP_CHECK(hipMemsetAsync(d->mcount.data(), 0, QEC_MC_NCOUNTERS_ALL * sizeof(unsigned long long), st));
     int rc = launch_mc_errors_syndrome(src, h, st);
     if (rc) return rc;
     if (ev0) QEC_HIP_CHECK(hipEventRecord(ev0, st));
@@ -915,8 +921,6 @@ int monte_carlo_part(qec_decoder* d, uint64_t seed, uint64_t start, uint64_t cou
     hipStream_t st = d->stream;
     int rc = mc_reserve(d, (size_t)std::min<uint64_t>(batch, std::max<uint64_t>(count, 1)), 0);
     if (rc) return rc;
-    // the counters and the fused pipeline's list lengths (zeroed again before every later batch)
-    QEC_HIP_CHECK(hipMemsetAsync(d->mcount.data(), 0, (QEC_MC_NCOUNTERS_ALL + mc_count_u64()) * sizeof(unsigned long long), st));
     // decode-kernel time from a ring of event pairs: the host waits only on a pair it reuses,
     // kRing batches behind the launches (no per-batch synchronisation)
     constexpr size_t kRing = 32;
@@ -940,6 +944,8 @@ int monte_carlo_part(qec_decoder* d, uint64_t seed, uint64_t start, uint64_t cou
         rc = mc_batch(d, h, MC_SRC_PHILOX, p, maxIter, stop, true, ev.ev[2 * slot], ev.ev[2 * slot + 1], k == 0);
         if (rc) return rc;
     }
+    if (k == 0)  // no batch zeroed the counters
+        QEC_HIP_CHECK(hipMemsetAsync(d->mcount.data(), 0, QEC_MC_NCOUNTERS_ALL * sizeof(unsigned long long), st));
     for (uint64_t j = k > kRing ? k - kRing : 0; j < k; ++j)
         if ((rc = harvest(j % kRing))) return rc;
     *decode_s = dec;

@@ -672,21 +672,25 @@ constexpr int kReduceGroups = 16;  // its first workgroups also add mc_fused_ker
 
 // One lane of an I-P check group (CheckLogicalError, Quantum_LDPC_Code.h:126-142, as
 // logical_from_columns): word k of the XOR of the I-P columns at the set bits of the residual res[0, nw)
-// (u32 words, record layout: x bits at [0, 8 nb), z bits from 8 nb) is nonzero.  Every lane of a group
-// walks the same residual; the columns are fetched four at a time.
+// (u32 words, record layout: x bits at [0, 8 nb), z bits from 8 nb; words: the mask of its nonzero
+// words) is nonzero.  Every lane of a group walks the same residual; the columns are fetched eight at
+// a time.
 template <int L, int P>
-__device__ __forceinline__ bool logical_group(const uint32_t* __restrict__ res, int nw, bool active,
+__device__ __forceinline__ bool logical_group(const uint32_t* __restrict__ res, uint64_t words, bool active,
                                               const uint64_t* __restrict__ cols, int cw, int k)
 {
     constexpr int n = L * P, nb = (n + 7) / 8;
+    constexpr int kBatch = 8;  // column fetches in flight
     uint64_t acc = 0;
     if (active && k < cw) {
-        for (int w = 0; w < nw; ++w) {
+        while (words) {  // the residual's nonzero words only
+            const int w = __builtin_ctzll(words);
+            words &= words - 1;
             uint32_t bits = res[w];
             while (bits) {
-                int q[4];
+                int q[kBatch];
 #pragma unroll
-                for (int u = 0; u < 4; ++u) {
+                for (int u = 0; u < kBatch; ++u) {
                     q[u] = -1;
                     if (bits) {
                         const int qq = 32 * w + __builtin_ctz(bits);
@@ -694,16 +698,16 @@ __device__ __forceinline__ bool logical_group(const uint32_t* __restrict__ res, 
                         q[u] = qq < 8 * nb ? qq : n + (qq - 8 * nb);
                     }
                 }
-                uint64_t c[4];
+                uint64_t c[kBatch];
 #pragma unroll
-                for (int u = 0; u < 4; ++u) c[u] = q[u] >= 0 ? cols[(size_t)q[u] * cw + k] : 0ull;
-                acc ^= (c[0] ^ c[1]) ^ (c[2] ^ c[3]);
+                for (int u = 0; u < kBatch; ++u) c[u] = q[u] >= 0 ? cols[(size_t)q[u] * cw + k] : 0ull;
+#pragma unroll
+                for (int u = 0; u < kBatch; ++u) acc ^= c[u];
             }
         }
     }
     return acc != 0ull;
 }
-
 
 template <int L, int P>
 __global__ __launch_bounds__(64 * kSurvWaves) void mc_survivor_kernel(const FusedArgs a)
@@ -757,6 +761,8 @@ __global__ __launch_bounds__(64 * kSurvWaves) void mc_survivor_kernel(const Fuse
         const uint32_t mw = valid ? a.merge[b] : 0u;
         const bool xclean = (mw & kXClean) != 0u;  // X residual 0; no X record words
         uint32_t nz = 0;
+        uint64_t nzw = 0;  // nonzero residual words
+        static_assert(kRW <= 64, "one mask bit per residual word");
 #pragma unroll
         for (int d = 0; d < kRW; ++d) {
             const uint32_t rv = valid ? r[d] : 0u;
@@ -767,6 +773,7 @@ __global__ __launch_bounds__(64 * kSurvWaves) void mc_survivor_kernel(const Fuse
             const uint32_t res = (mine[d] ^ rv) & m;
             mine[d] = res;
             nz |= res;
+            nzw |= (uint64_t)(res != 0u) << d;
         }
         // the flags: the list-mode decode ORs its sectors' into the merge word, which the fused kernel
         // set to the stopped sectors' (launch_decode_list, merge_only); the record's byte is not merged
@@ -782,8 +789,10 @@ __global__ __launch_bounds__(64 * kSurvWaves) void mc_survivor_kernel(const Fuse
                 need &= need - 1;
                 if (q == g) s = sl;
             }
-            const unsigned long long nzm = __ballot(logical_group<L, P>(region + (wv * 64 + (s < 0 ? 0 : s)) * RS, kRW, s >= 0,
-                                                                        a.imp_cols, a.imp_cw, k));
+            const int src = s < 0 ? 0 : s;
+            const uint64_t words = ((uint64_t)(uint32_t)__shfl((int)(nzw >> 32), src) << 32) | (uint32_t)__shfl((int)(uint32_t)nzw, src);
+            const unsigned long long nzm =
+                __ballot(logical_group<L, P>(region + (wv * 64 + src) * RS, words, s >= 0, a.imp_cols, a.imp_cw, k));
             unsigned long long p2 = pick;
             for (int q = 0; q < G && p2; ++q) {
                 const int sl = __builtin_ctzll(p2);

@@ -165,18 +165,20 @@ int qec_decoder_device(const qec_decoder* dec);         /* HIP device ordinal (o
  *   QEC_OPT_SCHEDULE (default 1): dispatch order of the wave-circulant launch.  Two small
  *     kernels (a counting sort) order the batch by syndrome weight and the decode waves take syndromes heaviest
  *     first, so the rare syndromes that run every iteration in full arithmetic start early
- *     instead of extending the launch (schedule.hip).  Outputs are written at each syndrome's
+ *     instead of extending the launch (schedule.hip); a sector-split launch orders each sector's
+ *     waves by that sector's weight.  Outputs are written at each syndrome's
  *     own index and are bit-identical either way.  0 = batch order, 1 = sorted when
  *     4096 <= B <= 2^22 (codes with one syndrome per wave, P > 32: 4096 <= B <= 2^19, above which
  *     the pass costs more than it saves), 2 = sorted when B <= 2^22, 3 = as 2 but with the one-launch
  *     local order for B <= 2^18 short-row codes (each chunk sorted in LDS, chunks interleaved by rank;
  *     measured slower than the global sort at P7 65 536, kept for experiments), 4 = as 2 but the
- *     global sort in one launch with a software grid barrier for up to 128 chunks (measured slower).  The workspace (5 B per syndrome + 1 MiB) is allocated
+ *     global sort in one launch with a software grid barrier for up to 128 chunks (measured slower).
+ *     The workspace (10 B per syndrome + 1 MiB) is allocated
  *     by qec_decoder_create for max_batch and grown on demand by larger calls.
  *   QEC_OPT_SECTOR_SPLIT (default 1): the X and Z sectors of a syndrome are decoded by two
  *     waves instead of one after the other (halves the longest wave).  The launch then zeroes
  *     flags[] first and each sector ORs in its bits.  Bit-identical either way.  0 = off,
- *     1 = the kernel variant's measured choice (P7: split waves below 2^19 syndromes; P61: sector
+ *     1 = the kernel variant's measured choice (P7: split waves up to 2^20 syndromes; P61: sector
  *     launches from 2^18 on), 2 = on where the variant has split kernels (the two shipped codes),
  *     3 = sector launches: two launches on the caller's stream, sector X then
  *     sector Z, each kernel compiled (and its registers allocated) for its own sector only; the Z

@@ -279,6 +279,7 @@ struct BpArgs {
     int32_t* iters;
     float* q;
     const int32_t* perm;  // dispatch order (schedule.hip): group slot k decodes syndrome perm[k]; null = batch order
+    int perm_sectors;     // perm holds the per-sector orders: the Z sector's waves take perm[B + k]
     // packed decision records (qec_decode_batch_packed_dev): per syndrome eX bits, eZ bits (nb bytes
     // each, bit j of byte k = qubit 8k + j), then the flags byte; null = byte outputs eX / eZ / flags
     uint8_t* rec;
@@ -1638,8 +1639,9 @@ void bp_decode_kernel(const BpArgs a)
     if (!__any(in_range)) return;
     // the syndrome index in 32 bits (launch_decode caps B below 2^31): a 64-bit index live across both
     // sectors spilled at 96 VGPRs
-    const uint32_t b = (in_range && a.perm != nullptr) ? (uint32_t)a.perm[slot] : (uint32_t)slot;
     const bool doX = MODE == 3 || (MODE != 4 && (!SPLIT || (wave & 1) == 0));  // wave-uniform
+    const long long pslot = (a.perm_sectors && !doX) ? slot + a.B : slot;
+    const uint32_t b = (in_range && a.perm != nullptr) ? (uint32_t)a.perm[pslot] : (uint32_t)slot;
     decode_group<RX, RZ, L, STOP, SH, TU, MODE>(a, tab0, stage, i, gb, b, in_range, doX);
 }
 
@@ -1921,11 +1923,14 @@ const void* select_variant(const Code& c, std::string& name)
 
 // QEC_OPT_SECTOR_SPLIT: 0 off, 1 the variant's tuned choice, 2 on (runtime-shift variants have
 // no split kernels: one wave per syndrome)
-// The tuned choice (split_auto) splits only batches below kSplitAutoMaxBatch: the two waves per
-// syndrome group help fill the chip when waves are few, and cost a merge per syndrome when they are
-// not (P7 fixed 20: 65 536 616 vs 512 M/s, 131 072 992 vs 846, 262 144 even, 524 288 1613 vs 1643,
-// 2^20 1790 vs 1835 M/s split vs one wave per group; profiles/r02/p7_split_r02s3zz.txt).
-constexpr long long kSplitAutoMaxBatch = 1LL << 19;
+// The tuned choice (split_auto) splits batches up to kSplitAutoMaxBatch: the two waves per syndrome
+// group help fill the chip when waves are few, and with each sector's waves in the order of that
+// sector's weight (schedule.hip, per-sector order) they also group like work: P7 fixed 20 at 2^19
+// 0.294 vs 0.342 ms, 2^20 0.500 vs 0.587 ms split vs one wave per group (round 2, total-weight
+// order: split lost from 2^19 on, profiles/r02/p7_split_r02s3zz.txt; round 4:
+// profiles/r04/cmp_sector_order_*.txt).  Above 2^20 the order pass has more chunks than the fused
+// scatter takes and falls back to the total-weight order.
+constexpr long long kSplitAutoMaxBatch = (1LL << 20) + 1;
 
 bool decode_uses_split(const void* variant, int stop, int split, long long B);
 // Sector launches (QEC_OPT_SECTOR_SPLIT = 3, or 1 from the variant's seq_min_batch on):
@@ -1957,7 +1962,7 @@ bool decode_has_phase_stats(const void* variant, int stop)
 int launch_decode(const void* variant, const Code& c, const uint8_t* sX, const uint8_t* sZ, bool sbits, long long B,
                   float errorProbability, int maxIter, int stop, uint8_t* eX, uint8_t* eZ, uint8_t* flags,
                   uint8_t* rec, int32_t* iters, float* q, int hardPaths, const int32_t* perm, int split,
-                  uint32_t* merge, bool merge_zeroed, hipStream_t stream, int rec_stride)
+                  uint32_t* merge, bool merge_zeroed, hipStream_t stream, int rec_stride, bool perm_sectors)
 {
     const Variant* v = static_cast<const Variant*>(variant);
     if (B <= 0) return QEC_OK;
@@ -1969,6 +1974,7 @@ int launch_decode(const void* variant, const Code& c, const uint8_t* sX, const u
     a.wZ = (c.mZ + 31) / 32;
     a.rec = rec;
     a.perm = perm;
+    a.perm_sectors = perm != nullptr && perm_sectors ? 1 : 0;
     const bool phase = (hardPaths & QEC_HP_PHASE) != 0;
     if (phase && v->phase[stop] == nullptr)
         return fail(QEC_ERR_UNSUPPORTED, "bp_decode: no phase-statistics kernel for this code");

@@ -18,12 +18,12 @@ const void* select_variant(const Code& c, std::string& name);
 int launch_decode(const void* variant, const Code& c, const uint8_t* sX, const uint8_t* sZ, bool sbits, long long B,
                   float errorProbability, int maxIter, int stop, uint8_t* eX, uint8_t* eZ, uint8_t* flags,
                   uint8_t* rec, int32_t* iters, float* q, int hardPaths, const int32_t* perm, int split,
-                  uint32_t* merge, bool merge_zeroed, hipStream_t stream, int rec_stride = 0);
+                  uint32_t* merge, bool merge_zeroed, hipStream_t stream, int rec_stride = 0, bool perm_sectors = false);
 size_t schedule_workspace_bytes(long long B, int mX, int mZ);
 long long schedule_max_batch();
 long long schedule_local_max_batch();
 int launch_schedule(const uint8_t* sX, const uint8_t* sZ, bool sbits, long long B, int mX, int mZ, void* ws,
-                    uint32_t* zero_merge, int32_t** perm_out, hipStream_t st, int method, uint32_t* bar);
+                    uint32_t* zero_merge, int32_t** perm_out, bool* sectors_out, hipStream_t st, int method, uint32_t* bar);
 bool decode_uses_split(const void* variant, int stop, int split, long long B);
 bool decode_needs_merge(const void* variant, int stop, int split, long long B);
 bool decode_has_list(const void* variant);
@@ -608,7 +608,7 @@ int dispatch_decode(qec_decoder* d, const uint8_t* sX, const uint8_t* sZ, long l
     const bool need_merge = !d->phase_stats && decode_needs_merge(d->variant, stop, d->sector_split, B);
     if (need_merge && (rc = ws_reserve(d->merge, (size_t)B, st, "decode"))) return rc;
     const int32_t* perm = nullptr;
-    bool zeroed = false;
+    bool zeroed = false, perm_sectors = false;
     const bool single = 2 * c.P > 64;  // one syndrome per wave
     const bool auto_on = B >= kScheduleMinBatch && (!single || B <= kScheduleMaxSingle) &&
                          !(stop == QEC_STOP_SYNDROME && p < kScheduleSyndromeMinP);
@@ -618,14 +618,14 @@ int dispatch_decode(qec_decoder* d, const uint8_t* sX, const uint8_t* sZ, long l
         int32_t* pm = nullptr;
         // a sector-split launch merges its flags in zeroed words: the order pass zeroes them
         const int method = d->schedule == 3 ? QEC_ORDER_LOCAL : d->schedule == 4 ? QEC_ORDER_ONE_LAUNCH : QEC_ORDER_GLOBAL;
-        rc = launch_schedule(sX, sZ, sbits, B, c.mX, c.mZ, d->sched.data(), split ? d->merge.data() : nullptr, &pm, st,
-                             method, d->gbar.data());
+        rc = launch_schedule(sX, sZ, sbits, B, c.mX, c.mZ, d->sched.data(), split ? d->merge.data() : nullptr, &pm,
+                             &perm_sectors, st, method, d->gbar.data());
         if (rc) return rc;
         perm = pm;
         zeroed = split;
     }
     rc = launch_decode(d->variant, c, sX, sZ, sbits, B, p, maxIter, stop, eX, eZ, flags, rec, iters, q, hp, perm,
-                       d->sector_split, need_merge ? d->merge.data() : nullptr, zeroed, st, rec_stride);
+                       d->sector_split, need_merge ? d->merge.data() : nullptr, zeroed, st, rec_stride, perm_sectors);
     if (rc) return rc;
     return ws_release(d, st);
 }

@@ -26,6 +26,7 @@
 //             prefixes, and places its syndromes (LDS atomics), perm[pos] = b.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 #include <cstdlib>
 
@@ -47,8 +48,12 @@ constexpr int kShortRows = 128;  // mX + mZ up to this many bytes: one thread pe
 constexpr int kMaxChunks = 1024;
 constexpr int kMaxChunk = 4096;
 #ifndef QEC_SCHED_FUSED_MAX
-#define QEC_SCHED_FUSED_MAX 128  // experiments: 0 always takes the separate offsets pass
+#define QEC_SCHED_FUSED_MAX 256  // experiments: 0 always takes the separate offsets pass
 #endif
+#ifndef QEC_SCHED_SECTORS
+#define QEC_SCHED_SECTORS 1  // sector-split launches: each sector's waves in the order of that sector's weight
+#endif
+constexpr bool kSchedSectors = QEC_SCHED_SECTORS;
 #ifndef QEC_SCHED_TARGET_CHUNKS
 #define QEC_SCHED_TARGET_CHUNKS 128  // chunks (histogram workgroups) aimed for when the batch is small
 #endif
@@ -229,14 +234,13 @@ struct FusedLds {
 };
 __device__ __forceinline__ void scatter_fused_body(const uint8_t* __restrict__ key, long long B, int chunk, int nch,
                                                    int nbk, const uint32_t* __restrict__ counts,
-                                                   int32_t* __restrict__ perm, FusedLds& s)
+                                                   int32_t* __restrict__ perm, FusedLds& s, int c)
 {
     uint32_t* tot = s.tot;
     uint32_t* pre = s.pre;
     uint32_t* start = s.start;
     uint32_t* cur = s.cur;
     const int t = threadIdx.x;
-    const int c = blockIdx.x;
     const int parts = kScatThreads / nbk;  // threads (k, part): bucket k's counts over chunks part, part + parts, ...
     const int k = t % nbk, part = t / nbk;
     if (part < parts) {
@@ -276,7 +280,79 @@ __global__ __launch_bounds__(kScatThreads) void schedule_scatter_fused_kernel(co
                                                                             int32_t* __restrict__ perm)
 {
     __shared__ FusedLds s;
-    scatter_fused_body(key, B, chunk, nch, nbk, counts, perm, s);
+    scatter_fused_body(key, B, chunk, nch, nbk, counts, perm, s, blockIdx.x);
+}
+
+// Per-sector order (QEC_SCHED_SECTORS, the sector-split launch): an X wave's work depends on the X
+// sector's weight alone and a Z wave's on the Z sector's, so each sector gets its own heaviest-first
+// order -- perm[0, B) for the X waves, perm[B, 2 B) for the Z waves -- from its own keys and counts
+// (X and Z in one histogram pass; the scatter's first nch workgroups place X, the others Z).  P7
+// fixed 20 (byte rows): 65 536 0.070 -> 0.059 ms, 262 144 0.185 -> 0.157 ms, and the split launch
+// now pays at 2^19 (0.342 -> 0.294 ms) and 2^20 (0.587 -> 0.500 ms, with up to 256 fused-scatter
+// chunks); P61 65 536 split +1.5 %, 131 072 -2 % (it keeps one wave per syndrome)
+// (profiles/r04/cmp_sector_order_*.txt).
+template <int SPLIT, bool BITS>
+__global__ __launch_bounds__(kHistThreads) void schedule_hist_sec_kernel(const uint8_t* __restrict__ sX,
+                                                                       const uint8_t* __restrict__ sZ, long long B,
+                                                                       int mX, int mZ, int chunk, int nbk,
+                                                                       uint8_t* __restrict__ keyX,
+                                                                       uint32_t* __restrict__ countsX,
+                                                                       uint32_t* __restrict__ zero_merge)
+{
+    __shared__ uint32_t hX[kBuckets], hZ[kBuckets];
+    const long long nch = gridDim.x;
+    uint8_t* __restrict__ keyZ = keyX + B;
+    uint32_t* __restrict__ countsZ = countsX + nch * nbk;
+    const int t = threadIdx.x;
+    const int q = t % SPLIT;
+    const long long r0 = (long long)blockIdx.x * chunk;
+    const long long r1 = r0 + chunk < B ? r0 + chunk : B;
+    if (t < kBuckets) hX[t] = hZ[t] = 0;
+    __syncthreads();
+    for (long long b = r0 + t / SPLIT; b - (t / SPLIT) < r1; b += blockDim.x / SPLIT) {
+        uint32_t wx = 0, wz = 0;
+        if (b < r1) {
+            if constexpr (BITS) {  // mX, mZ: words per row
+                const uint32_t* x = reinterpret_cast<const uint32_t*>(sX) + b * mX;
+                const uint32_t* z = reinterpret_cast<const uint32_t*>(sZ) + b * mZ;
+                for (int k = 0; k < mX; ++k) wx += __popc(x[k]);
+                for (int k = 0; k < mZ; ++k) wz += __popc(z[k]);
+            } else {
+                wx = range_weight(sX, b * mX + (long long)(mX * q / SPLIT), b * mX + (long long)(mX * (q + 1) / SPLIT));
+                wz = range_weight(sZ, b * mZ + (long long)(mZ * q / SPLIT), b * mZ + (long long)(mZ * (q + 1) / SPLIT));
+            }
+        }
+#pragma unroll
+        for (int o = 1; o < SPLIT; o <<= 1) {
+            wx += __shfl_xor(wx, o);
+            wz += __shfl_xor(wz, o);
+        }
+        if (q == 0 && b < r1) {
+            const int kx = nbk - 1 - (int)(wx < (uint32_t)nbk - 1 ? wx : (uint32_t)nbk - 1);
+            const int kz = nbk - 1 - (int)(wz < (uint32_t)nbk - 1 ? wz : (uint32_t)nbk - 1);
+            keyX[b] = (uint8_t)kx;
+            keyZ[b] = (uint8_t)kz;
+            atomicAdd(&hX[kx], 1u);
+            atomicAdd(&hZ[kz], 1u);
+            if (zero_merge) zero_merge[b] = 0u;
+        }
+    }
+    __syncthreads();
+    if (t < nbk) {
+        countsX[(long long)blockIdx.x * nbk + t] = hX[t];
+        countsZ[(long long)blockIdx.x * nbk + t] = hZ[t];
+    }
+}
+
+__global__ __launch_bounds__(kScatThreads) void schedule_scatter_sec_kernel(const uint8_t* __restrict__ keyX, long long B,
+                                                                          int chunk, int nch, int nbk,
+                                                                          const uint32_t* __restrict__ countsX,
+                                                                          int32_t* __restrict__ perm)
+{
+    __shared__ FusedLds s;
+    const int sec = (int)blockIdx.x >= nch ? 1 : 0;
+    scatter_fused_body(keyX + sec * B, B, chunk, nch, nbk, countsX + (long long)sec * nch * nbk, perm + sec * B, s,
+                       (int)blockIdx.x - sec * nch);
 }
 
 // (A cooperative single launch -- histogram, grid barrier, scatter -- was measured 4x slower than the
@@ -333,7 +409,7 @@ __global__ __launch_bounds__(kScatThreads) void schedule_one_launch_kernel(const
     else
         hist_body<MODE == 1 ? 1 : kHistSplitLong>(sX, sZ, B, mX, mZ, chunk, nbk, key, counts, zero_merge, h);
     grid_arrive_wait(bar, (uint32_t)nch);
-    scatter_fused_body(key, B, chunk, nch, nbk, counts, perm, s);
+    scatter_fused_body(key, B, chunk, nch, nbk, counts, perm, s, blockIdx.x);
     grid_depart(bar, (uint32_t)nch);
 }
 
@@ -421,21 +497,25 @@ static int chunk_of(long long B, int min_chunk, int max_chunk, int* nchunks)
 // B <= kMaxChunks * kMaxChunk syndromes per ordered launch (4 M)
 long long schedule_max_batch() { return (long long)kMaxChunks * kMaxChunk; }
 
-// workspace layout: perm [B] i32, counts [chunks][256] u32, totals [256] u32, key [B] u8
-static size_t perm_bytes(long long B) { return ((size_t)B * sizeof(int32_t) + 255) & ~(size_t)255; }
+// workspace layout: perm [2 B] i32 (the per-sector order takes both halves), counts [chunks][256] u32
+// (per-sector: X then Z, [nch][nbk] each, at most kMaxFusedChunks chunks), totals [256] u32, key [2 B] u8
+static size_t perm_bytes(long long B) { return ((size_t)2 * B * sizeof(int32_t) + 255) & ~(size_t)255; }
 
 size_t schedule_workspace_bytes(long long B, int, int)
 {
-    return perm_bytes(B) + (size_t)kMaxChunks * kBuckets * 4 + kBuckets * 4 + B + 64;
+    return perm_bytes(B) + (size_t)kMaxChunks * kBuckets * 4 + kBuckets * 4 + 2 * B + 64;
 }
 
 // Fills the workspace (schedule_workspace_bytes bytes) and returns in *perm_out the
 // heaviest-first order of the batch.  zero_merge (nullable): B words the hist pass zeroes on
-// the way (the sector-split decode merges its two sectors' flags there, bp_decode.hip).  bar
-// (nullable): the handle's two zeroed grid-barrier words (schedule_one_launch_kernel).
+// the way (the sector-split decode merges its two sectors' flags there, bp_decode.hip); a
+// sector-split launch may get the per-sector order instead (*sectors_out = true: 2 B entries, the
+// Z waves' order from perm[B]).  bar (nullable): the handle's two zeroed grid-barrier words
+// (schedule_one_launch_kernel).
 int launch_schedule(const uint8_t* sX, const uint8_t* sZ, bool sbits, long long B, int mX, int mZ, void* ws,
-                    uint32_t* zero_merge, int32_t** perm_out, hipStream_t st, int method, uint32_t* bar)
+                    uint32_t* zero_merge, int32_t** perm_out, bool* sectors_out, hipStream_t st, int method, uint32_t* bar)
 {
+    *sectors_out = false;
     if (B > schedule_max_batch()) return fail(QEC_ERR_ARG, "schedule: batch too large to order");
     const bool shortrows = sbits || mX + mZ <= kShortRows;
     if (method == QEC_ORDER_LOCAL && shortrows && B <= schedule_local_max_batch()) {
@@ -478,6 +558,24 @@ int launch_schedule(const uint8_t* sX, const uint8_t* sZ, bool sbits, long long 
     // buckets: weights 0 .. mX + mZ (fused pass), 256 for the separate offsets / scatter passes
     int nbk = kBuckets;
     if (fused && mX + mZ + 1 < kBuckets) nbk = mX + mZ + 1 < 32 ? 32 : mX + mZ + 1;
+    if (kSchedSectors && method == QEC_ORDER_GLOBAL && zero_merge != nullptr && fused) {
+        const int nbs = std::max(32, std::min(kBuckets, std::max(mX, mZ) + 1));  // sector weights 0 .. max(mX, mZ)
+        if (sbits)
+            hipLaunchKernelGGL((schedule_hist_sec_kernel<1, true>), dim3(nch), dim3(hthreads), 0, st, sX, sZ, B, (mX + 31) / 32,
+                               (mZ + 31) / 32, chunk, nbs, key, counts, zero_merge);
+        else if (shortrows)
+            hipLaunchKernelGGL((schedule_hist_sec_kernel<1, false>), dim3(nch), dim3(hthreads), 0, st, sX, sZ, B, mX, mZ, chunk,
+                               nbs, key, counts, zero_merge);
+        else
+            hipLaunchKernelGGL((schedule_hist_sec_kernel<kHistSplitLong, false>), dim3(nch), dim3(hthreads), 0, st, sX, sZ, B,
+                               mX, mZ, chunk, nbs, key, counts, zero_merge);
+        hipLaunchKernelGGL(schedule_scatter_sec_kernel, dim3(2 * nch), dim3(kScatThreads), 0, st, key, B, chunk, nch, nbs,
+                           counts, perm);
+        const hipError_t err = hipGetLastError();
+        if (err != hipSuccess) return fail(QEC_ERR_HIP, std::string("schedule launch: ") + hipGetErrorString(err));
+        *sectors_out = true;
+        return QEC_OK;
+    }
     if (method == QEC_ORDER_ONE_LAUNCH && fused && bar != nullptr && nch <= kOneLaunchChunks) {
         // histogram, grid barrier, offsets and scatter in one launch (schedule_one_launch_kernel)
         if (sbits)

@@ -20,10 +20,11 @@ int launch_decode(const void* variant, const Code& c, const uint8_t* sX, const u
                   uint8_t* rec, int32_t* iters, float* q, int hardPaths, const int32_t* perm, int split,
                   uint32_t* merge, bool merge_zeroed, hipStream_t stream, int rec_stride = 0, bool perm_sectors = false);
 size_t schedule_workspace_bytes(long long B, int mX, int mZ);
+bool schedule_sector_order(long long B, bool sbits, int mX, int mZ);
 long long schedule_max_batch();
 long long schedule_local_max_batch();
 int launch_schedule(const uint8_t* sX, const uint8_t* sZ, bool sbits, long long B, int mX, int mZ, void* ws,
-                    uint32_t* zero_merge, int32_t** perm_out, bool* sectors_out, hipStream_t st, int method, uint32_t* bar);
+                    uint32_t* zero_merge, bool want_sectors, int32_t** perm_out, bool* sectors_out, hipStream_t st, int method, uint32_t* bar);
 bool decode_uses_split(const void* variant, int stop, int split, long long B);
 bool decode_needs_merge(const void* variant, int stop, int split, long long B);
 bool decode_has_list(const void* variant);
@@ -532,7 +533,9 @@ namespace {
 // tail to remove and the pass is pure cost: below kScheduleSyndromeMinP it stays off there
 // (P61, 65 536 per batch: p = 0.001 290 vs 266 M/s, 0.002 263 vs 257 off vs on, but 0.005 190 vs
 // 197, 0.01 124 vs 143; 262 144 at p = 0.002: 0.450 vs 0.521 ms; profiles/r02/psweep_sched{0,1}_r02s3g.json,
-// profiles/r02/cmp_options_r02s3zb.txt).
+// profiles/r02/cmp_options_r02s3zb.txt).  With sector launches or split waves each sector's waves
+// can follow that sector's own weight (schedule_sector_order), which pays for P61 at 2^20 too: the
+// bit-row headline 143.1 vs 140.6 M/s ordered vs not (profiles/r04/bench/configs3_*).
 constexpr long long kScheduleMinBatch = 4096;
 constexpr long long kScheduleMaxSingle = 1LL << 19;
 constexpr float kScheduleSyndromeMinP = 0.004f;
@@ -610,7 +613,9 @@ int dispatch_decode(qec_decoder* d, const uint8_t* sX, const uint8_t* sZ, long l
     const int32_t* perm = nullptr;
     bool zeroed = false, perm_sectors = false;
     const bool single = 2 * c.P > 64;  // one syndrome per wave
-    const bool auto_on = B >= kScheduleMinBatch && (!single || B <= kScheduleMaxSingle) &&
+    const bool sectors = split || need_merge;  // split waves or sector launches
+    const bool auto_on = B >= kScheduleMinBatch &&
+                         (!single || B <= kScheduleMaxSingle || (sectors && schedule_sector_order(B, sbits, c.mX, c.mZ))) &&
                          !(stop == QEC_STOP_SYNDROME && p < kScheduleSyndromeMinP);
     if (B > 1 && B <= schedule_max_batch() && (d->schedule >= 2 || (d->schedule == 1 && auto_on))) {
         if ((rc = ws_reserve(d->sched, schedule_workspace_bytes(B, c.mX, c.mZ), st, "decode: dispatch order")))
@@ -618,8 +623,9 @@ int dispatch_decode(qec_decoder* d, const uint8_t* sX, const uint8_t* sZ, long l
         int32_t* pm = nullptr;
         // a sector-split launch merges its flags in zeroed words: the order pass zeroes them
         const int method = d->schedule == 3 ? QEC_ORDER_LOCAL : d->schedule == 4 ? QEC_ORDER_ONE_LAUNCH : QEC_ORDER_GLOBAL;
-        rc = launch_schedule(sX, sZ, sbits, B, c.mX, c.mZ, d->sched.data(), split ? d->merge.data() : nullptr, &pm,
-                             &perm_sectors, st, method, d->gbar.data());
+        // each sector's waves in the order of its own weight: split waves, or sector launches (need_merge alone)
+        rc = launch_schedule(sX, sZ, sbits, B, c.mX, c.mZ, d->sched.data(), split ? d->merge.data() : nullptr, sectors,
+                             &pm, &perm_sectors, st, method, d->gbar.data());
         if (rc) return rc;
         perm = pm;
         zeroed = split;

@@ -497,6 +497,16 @@ static int chunk_of(long long B, int min_chunk, int max_chunk, int* nchunks)
 // B <= kMaxChunks * kMaxChunk syndromes per ordered launch (4 M)
 long long schedule_max_batch() { return (long long)kMaxChunks * kMaxChunk; }
 
+// whether a batch of B syndromes that asks for it gets the per-sector order (its chunks fit the fused scatter)
+bool schedule_sector_order(long long B, bool sbits, int mX, int mZ)
+{
+    if (!kSchedSectors || B <= 1 || B > schedule_max_batch()) return false;
+    const bool shortrows = sbits || mX + mZ <= kShortRows;
+    int nch = 0;
+    chunk_of(B, 256, shortrows ? 4 * kHistThreads : 512, &nch);
+    return nch <= kMaxFusedChunks;
+}
+
 // workspace layout: perm [2 B] i32 (the per-sector order takes both halves), counts [chunks][256] u32
 // (per-sector: X then Z, [nch][nbk] each, at most kMaxFusedChunks chunks), totals [256] u32, key [2 B] u8
 static size_t perm_bytes(long long B) { return ((size_t)2 * B * sizeof(int32_t) + 255) & ~(size_t)255; }
@@ -508,12 +518,13 @@ size_t schedule_workspace_bytes(long long B, int, int)
 
 // Fills the workspace (schedule_workspace_bytes bytes) and returns in *perm_out the
 // heaviest-first order of the batch.  zero_merge (nullable): B words the hist pass zeroes on
-// the way (the sector-split decode merges its two sectors' flags there, bp_decode.hip); a
-// sector-split launch may get the per-sector order instead (*sectors_out = true: 2 B entries, the
-// Z waves' order from perm[B]).  bar (nullable): the handle's two zeroed grid-barrier words
+// the way (the sector-split decode merges its two sectors' flags there, bp_decode.hip).
+// want_sectors (sector-split waves or sector launches): the per-sector order where the fused scatter
+// takes the batch (*sectors_out = true: 2 B entries, the Z waves' order from perm[B]).  bar (nullable): the handle's two zeroed grid-barrier words
 // (schedule_one_launch_kernel).
 int launch_schedule(const uint8_t* sX, const uint8_t* sZ, bool sbits, long long B, int mX, int mZ, void* ws,
-                    uint32_t* zero_merge, int32_t** perm_out, bool* sectors_out, hipStream_t st, int method, uint32_t* bar)
+                    uint32_t* zero_merge, bool want_sectors, int32_t** perm_out, bool* sectors_out, hipStream_t st,
+                    int method, uint32_t* bar)
 {
     *sectors_out = false;
     if (B > schedule_max_batch()) return fail(QEC_ERR_ARG, "schedule: batch too large to order");
@@ -558,7 +569,7 @@ int launch_schedule(const uint8_t* sX, const uint8_t* sZ, bool sbits, long long 
     // buckets: weights 0 .. mX + mZ (fused pass), 256 for the separate offsets / scatter passes
     int nbk = kBuckets;
     if (fused && mX + mZ + 1 < kBuckets) nbk = mX + mZ + 1 < 32 ? 32 : mX + mZ + 1;
-    if (kSchedSectors && method == QEC_ORDER_GLOBAL && zero_merge != nullptr && fused) {
+    if (kSchedSectors && method == QEC_ORDER_GLOBAL && want_sectors && fused) {
         const int nbs = std::max(32, std::min(kBuckets, std::max(mX, mZ) + 1));  // sector weights 0 .. max(mX, mZ)
         if (sbits)
             hipLaunchKernelGGL((schedule_hist_sec_kernel<1, true>), dim3(nch), dim3(hthreads), 0, st, sX, sZ, B, (mX + 31) / 32,

@@ -140,6 +140,21 @@ def test_monte_carlo_shards_add_up(env):
         assert whole[k] == a[k] + b[k], k
 
 
+def test_monte_carlo_fused_batches_and_empty_run(env):
+    """The fused low-p pipeline over several batches of one call (the list lengths are zeroed again
+    before every later batch; the first batch's memset also zeroes the counters) adds up to one
+    batch, and a run of zero samples right after returns zero counters, not the last run's."""
+    code, dec, _ = env["P61"]
+    one = dec.monte_carlo(11, 0, 10000, 0.002, 50, "syndrome", batch=10000)
+    many = dec.monte_carlo(11, 0, 10000, 0.002, 50, "syndrome", batch=4096)
+    for k in q.MC_COUNTERS + ("tested", "iterationsX", "iterationsZ"):
+        assert one[k] == many[k], k
+    assert one["withX"] > 0 and one["corrected"] > 0
+    empty = dec.monte_carlo(11, 0, 0, 0.002, 50, "syndrome")
+    for k in q.MC_COUNTERS + ("tested", "iterationsX", "iterationsZ"):
+        assert empty[k] == 0, k
+
+
 def test_monte_carlo_full_batch(env):
     """qec_monte_carlo at psweep's default shape (2^20 samples in one batch: 64-lane front-end waves,
     one decode launch) against oracle counting on its last 2 048 samples (the same launch shape minus

@@ -310,15 +310,15 @@ def test_schedule_many_chunks_identical(env, key):
 
 @pytest.mark.parametrize("key,B", [("P7", 70001), ("P7", 600001), ("P61", 70001)])
 def test_per_sector_order_identical(env, key, B):
-    """The sector-split launch takes each sector's waves in the order of that sector's weight
-    (schedule.hip, perm[0, B) for X and perm[B, 2 B) for Z; P7 600 001 spreads the order pass over
-    147 chunks of the fused scatter): the same bits as one wave per syndrome group in total-weight
-    order and as batch order."""
+    """The sector-split launch (split waves, 2, or sector launches, 3) takes each sector's waves in
+    the order of that sector's weight (schedule.hip, perm[0, B) for X and perm[B, 2 B) for Z; P7
+    600 001 spreads the order pass over 147 chunks of the fused scatter): the same bits as one wave
+    per syndrome group in total-weight order and as batch order."""
     code, dec, _ = env[key]
     x, z = depolarizing_errors(code.n, 7 + B, B, 0.03)
     sX, sZ = code.syndrome(0, x), code.syndrome(1, z)
     outs = []
-    for sched, split in ((2, 2), (2, 0), (0, 2), (0, 0)):
+    for sched, split in ((2, 2), (2, 3), (2, 0), (0, 2), (0, 0)):
         dec.set_option("schedule", sched)
         dec.set_option("sector_split", split)
         try:

@@ -152,17 +152,26 @@ def main():
                     help="only the timed steps (profiling runs: no full-arithmetic / phase / sustained re-timings)")
     args = ap.parse_args()
 
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ and "RANK" not in os.environ:
+        # `python bench.py --gpus N` without a launcher: start the N ranks (one process per GPU) under
+        # torch.distributed.run as children, before anything here touches a GPU, and pass on their
+        # exit status; rank 0 prints the JSON line
+        sys.exit(relaunch(args.gpus))
+    if world != args.gpus:
+        print("bench.py: --gpus %d but WORLD_SIZE %d: refusing to report a %d-GPU run as %d" %
+              (args.gpus, world, world, args.gpus), file=sys.stderr)
+        sys.exit(2)
+
     import torch
     import torch.distributed as dist
 
     import qec_ldpc_amd as q
     from qec_ldpc_amd.codes import code_path
+    from qec_ldpc_amd.synthetic import bit_rows
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and rank == 0:
-        print("warning: --gpus %d but WORLD_SIZE %d; using WORLD_SIZE" % (args.gpus, world), file=sys.stderr)
     backend = None
     if world > 1:
         # RCCL ("nccl") over xGMI; QEC_BENCH_BACKEND=gloo rehearses the multi-rank path with
@@ -341,6 +350,19 @@ def main():
         print(json.dumps(out), flush=True)
 
 
+def relaunch(nproc):
+    """Runs this script under `python -m torch.distributed.run --nproc-per-node nproc` (rendezvous on
+    127.0.0.1) as a child process with the same arguments; returns its exit status."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.run(cmd).returncode
+
+
 def timed_steps(step, steps, stream, dev, world):
     """K steps between barrier + synchronize on both sides; wall time max over ranks, and the
     mean decode-launch time from HIP events on the launch stream."""
@@ -398,17 +420,6 @@ def valu_roofline(pm, path, B, kernel_ms):
     if pm.get("lds_issue_frac") is not None and pm.get("kernel_trace_avg_ns"):
         base["lds_issue_frac"] = round(pm["lds_issue_frac"] * pm["kernel_trace_avg_ns"] * 1e-6 / kernel_ms, 4)
     return base
-
-
-def bit_rows(s):
-    """[B, m] 0/1 bytes -> [B, ceil(m / 32)] int32 words, bit c of word c / 32 = check c."""
-    import torch
-    B, m = s.shape
-    w = -(-m // 32)
-    pad = torch.zeros((B, 32 * w), dtype=torch.int64, device=s.device)
-    pad[:, :m] = (s != 0).to(torch.int64)
-    v = (pad.view(B, w, 32) << torch.arange(32, device=s.device, dtype=torch.int64)).sum(2)
-    return torch.where(v >= 2 ** 31, v - 2 ** 32, v).to(torch.int32).contiguous()
 
 
 def retime_step(step, stream, B, outs, reps=3, world=1):

@@ -196,9 +196,22 @@ int qec_decoder_device(const qec_decoder* dec);         /* HIP device ordinal (o
  *     sectors go on and the ordered decode of the whole batch is faster), 2 = always, 3 = as 1
  *     without the fused form.  Fused form (1, 2; depolarising qec_monte_carlo runs): sampler,
  *     syndromes, triage and the finished samples' statistics in one kernel, so only the samples
- *     with a sector that goes on reach HBM (list-mode decode, then their statistics). */
+ *     with a sector that goes on reach HBM (list-mode decode, then their statistics).
+ *   QEC_OPT_LAST_PATH (read only; qec_decoder_set_option refuses it): the launch sequence the
+ *     handle's last decode call enqueued, as QEC_PATH_* bits (0 before the first decode), so a test
+ *     can assert which kernels its comparison went through. */
 enum { QEC_OPT_HARD_PATHS = 1, QEC_OPT_CYCLE_JUMP = 2, QEC_OPT_SCHEDULE = 3, QEC_OPT_SECTOR_SPLIT = 4,
-       QEC_OPT_PHASE_STATS = 5, QEC_OPT_TRIAGE = 6 };
+       QEC_OPT_PHASE_STATS = 5, QEC_OPT_TRIAGE = 6, QEC_OPT_LAST_PATH = 7 };
+enum {
+    QEC_PATH_ORDERED = 1,          /* dispatch order pass (schedule.hip) */
+    QEC_PATH_SECTOR_ORDER = 2,     /* ... in the per-sector form (each sector's waves by its own weight) */
+    QEC_PATH_SPLIT_WAVES = 4,      /* X and Z sectors in separate waves of one launch */
+    QEC_PATH_SECTOR_LAUNCHES = 8,  /* an X launch, then a Z launch */
+    QEC_PATH_TRIAGE = 16,          /* iteration-0 triage + list-mode decode */
+    QEC_PATH_BIT_ROWS = 32,        /* bit-row syndromes in */
+    QEC_PATH_SPARSE = 64,          /* sparse-graph engine */
+    QEC_PATH_RECORDS = 128         /* packed decision records out */
+};
 int qec_decoder_set_option(qec_decoder* dec, int option, int value);
 int qec_decoder_get_option(const qec_decoder* dec, int option, int* value);
 /* which kernel variant serves this code: writes a short name (e.g. "wave-circulant P=61 G=1") */

@@ -26,7 +26,11 @@ CONVERGENCE_FAIL_X = 4
 CONVERGENCE_FAIL_Z = 8
 STOP = {"ref": 0, "fixed": 1, "syndrome": 2}
 ENGINE = {"auto": 0, "circulant": 1, "sparse": 2, "cpu": 3}
-OPTION = {"hard_paths": 1, "cycle_jump": 2, "schedule": 3, "sector_split": 4, "phase_stats": 5, "triage": 6}
+OPTION = {"hard_paths": 1, "cycle_jump": 2, "schedule": 3, "sector_split": 4, "phase_stats": 5, "triage": 6,
+          "last_path": 7}
+# QEC_PATH_* bits of QEC_OPT_LAST_PATH (include/qec_ldpc.h): the launch sequence of the last decode call
+PATH = {"ordered": 1, "sector_order": 2, "split_waves": 4, "sector_launches": 8, "triage": 16, "bit_rows": 32,
+        "sparse": 64, "records": 128}
 
 # every symbol include/qec_ldpc.h declares
 EXPORTS = (
@@ -342,6 +346,12 @@ class DecoderGPU:
         v = ctypes.c_int(0)
         _check(lib().qec_decoder_get_option(self._h, OPTION[name], ctypes.byref(v)), "qec_decoder_get_option")
         return v.value
+
+    def last_path(self):
+        """The launch sequence of this handle's last decode call (QEC_OPT_LAST_PATH) as a set of
+        PATH names, e.g. {"bit_rows", "records", "ordered", "sector_order", "sector_launches"}."""
+        v = self.get_option("last_path")
+        return {k for k, b in PATH.items() if v & b}
 
     def record_bytes(self):
         """Bytes of one packed decision record: 2 ceil(n/8) + 1."""

@@ -114,6 +114,7 @@ struct qec_decoder {
     int sector_split = 1;           // QEC_OPT_SECTOR_SPLIT (0 off, 1 auto, 2 split waves, 3 sector launches)
     int phase_stats = 0;            // QEC_OPT_PHASE_STATS
     int triage = 1;                 // QEC_OPT_TRIAGE
+    int last_path = 0;              // QEC_OPT_LAST_PATH: QEC_PATH_* bits of the last decode call
     // workspace shared by every launch of this handle (dispatch order, split-flag merge words,
     // sparse byte staging for packed output); ws_ev marks the last launch that used it, so a call
     // on another stream waits for it (stream-ordered reuse)
@@ -501,6 +502,7 @@ int qec_decoder_set_option(qec_decoder* d, int option, int value)
         if (value < 0 || value > 3) return fail(QEC_ERR_ARG, "qec_decoder_set_option: QEC_OPT_TRIAGE is 0 .. 3");
         d->triage = value;
         return QEC_OK;
+    case QEC_OPT_LAST_PATH: return fail(QEC_ERR_ARG, "qec_decoder_set_option: QEC_OPT_LAST_PATH is read only");
     default: return fail(QEC_ERR_ARG, "qec_decoder_set_option: unknown option");
     }
 }
@@ -515,6 +517,7 @@ int qec_decoder_get_option(const qec_decoder* d, int option, int* value)
     case QEC_OPT_SECTOR_SPLIT: *value = d->sector_split; return QEC_OK;
     case QEC_OPT_PHASE_STATS: *value = d->phase_stats; return QEC_OK;
     case QEC_OPT_TRIAGE: *value = d->triage; return QEC_OK;
+    case QEC_OPT_LAST_PATH: *value = d->parts.empty() ? d->last_path : d->parts[0]->last_path; return QEC_OK;
     default: return fail(QEC_ERR_ARG, "qec_decoder_get_option: unknown option");
     }
 }
@@ -540,6 +543,8 @@ constexpr long long kScheduleMinBatch = 4096;
 constexpr long long kScheduleMaxSingle = 1LL << 19;
 constexpr float kScheduleSyndromeMinP = 0.004f;
 constexpr float kTriageMaxP = 0.01f;  // QEC_OPT_TRIAGE = 1 triages syndrome-stop batches up to this p
+// QEC_OPT_SECTOR_SPLIT = 1 splits batches above this size only when they get the per-sector order
+constexpr long long kSplitOrderedMinBatch = 1LL << 19;
 
 int hard_path_bits(const qec_decoder* d)
 {
@@ -566,7 +571,9 @@ int dispatch_decode(qec_decoder* d, const uint8_t* sX, const uint8_t* sZ, long l
     const Code& c = *d->code;
     int rc = ws_acquire(d, st);
     if (rc) return rc;
+    d->last_path = (sbits ? QEC_PATH_BIT_ROWS : 0) | (rec != nullptr ? QEC_PATH_RECORDS : 0);
     if (d->engine == QEC_ENGINE_SPARSE) {
+        d->last_path |= QEC_PATH_SPARSE;
         if (sbits) return fail(QEC_ERR_UNSUPPORTED, "decode: bit-row syndromes need the wave-circulant engine");
         if (rec_stride > 0 && rec_stride != 2 * ((c.n + 7) / 8) + 1)
             return fail(QEC_ERR_UNSUPPORTED, "decode: padded record rows need the wave-circulant engine");
@@ -605,24 +612,36 @@ int dispatch_decode(qec_decoder* d, const uint8_t* sX, const uint8_t* sZ, long l
             rc = launch_decode_list(d->variant, c, sX, sZ, B, p, maxIter, hp, rec, iters, d->merge.data(), lX, lZ, cnt, st,
                                     rec_stride, false, 1);
         if (rc) return rc;
+        d->last_path |= QEC_PATH_TRIAGE;
         return ws_release(d, st);
     }
-    const bool split = !d->phase_stats && decode_uses_split(d->variant, stop, d->sector_split, B);
-    const bool need_merge = !d->phase_stats && decode_needs_merge(d->variant, stop, d->sector_split, B);
-    if (need_merge && (rc = ws_reserve(d->merge, (size_t)B, st, "decode"))) return rc;
-    const int32_t* perm = nullptr;
-    bool zeroed = false, perm_sectors = false;
+    int split_opt = d->sector_split;
+    bool split = !d->phase_stats && decode_uses_split(d->variant, stop, split_opt, B);
+    bool need_merge = !d->phase_stats && decode_needs_merge(d->variant, stop, split_opt, B);
     const bool single = 2 * c.P > 64;  // one syndrome per wave
-    const bool sectors = split || need_merge;  // split waves or sector launches
+    bool sectors = split || need_merge;  // split waves or sector launches
     const bool auto_on = B >= kScheduleMinBatch &&
                          (!single || B <= kScheduleMaxSingle || (sectors && schedule_sector_order(B, sbits, c.mX, c.mZ))) &&
                          !(stop == QEC_STOP_SYNDROME && p < kScheduleSyndromeMinP);
-    if (B > 1 && B <= schedule_max_batch() && (d->schedule >= 2 || (d->schedule == 1 && auto_on))) {
+    const bool ordered = B > 1 && B <= schedule_max_batch() && (d->schedule >= 2 || (d->schedule == 1 && auto_on));
+    const int method = d->schedule == 3 ? QEC_ORDER_LOCAL : d->schedule == 4 ? QEC_ORDER_ONE_LAUNCH : QEC_ORDER_GLOBAL;
+    // The tuned split above kSplitOrderedMinBatch was measured only with the per-sector order (round 2:
+    // in total-weight order one wave per group won from 2^19 on); without that order keep one wave per group
+    if (split && split_opt == 1 && B > kSplitOrderedMinBatch &&
+        !(ordered && method == QEC_ORDER_GLOBAL && schedule_sector_order(B, sbits, c.mX, c.mZ))) {
+        split_opt = 0;
+        split = false;
+        need_merge = !d->phase_stats && decode_needs_merge(d->variant, stop, split_opt, B);
+        sectors = need_merge;
+    }
+    if (need_merge && (rc = ws_reserve(d->merge, (size_t)B, st, "decode"))) return rc;
+    const int32_t* perm = nullptr;
+    bool zeroed = false, perm_sectors = false;
+    if (ordered) {
         if ((rc = ws_reserve(d->sched, schedule_workspace_bytes(B, c.mX, c.mZ), st, "decode: dispatch order")))
             return rc;
         int32_t* pm = nullptr;
         // a sector-split launch merges its flags in zeroed words: the order pass zeroes them
-        const int method = d->schedule == 3 ? QEC_ORDER_LOCAL : d->schedule == 4 ? QEC_ORDER_ONE_LAUNCH : QEC_ORDER_GLOBAL;
         // each sector's waves in the order of its own weight: split waves, or sector launches (need_merge alone)
         rc = launch_schedule(sX, sZ, sbits, B, c.mX, c.mZ, d->sched.data(), split ? d->merge.data() : nullptr, sectors,
                              &pm, &perm_sectors, st, method, d->gbar.data());
@@ -631,8 +650,10 @@ int dispatch_decode(qec_decoder* d, const uint8_t* sX, const uint8_t* sZ, long l
         zeroed = split;
     }
     rc = launch_decode(d->variant, c, sX, sZ, sbits, B, p, maxIter, stop, eX, eZ, flags, rec, iters, q, hp, perm,
-                       d->sector_split, need_merge ? d->merge.data() : nullptr, zeroed, st, rec_stride, perm_sectors);
+                       split_opt, need_merge ? d->merge.data() : nullptr, zeroed, st, rec_stride, perm_sectors);
     if (rc) return rc;
+    d->last_path |= (perm ? QEC_PATH_ORDERED : 0) | (perm && perm_sectors ? QEC_PATH_SECTOR_ORDER : 0) |
+                    (split ? QEC_PATH_SPLIT_WAVES : 0) | (need_merge && !split ? QEC_PATH_SECTOR_LAUNCHES : 0);
     return ws_release(d, st);
 }
 

@@ -27,6 +27,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdint>
 #include <cstdlib>
 
@@ -360,9 +361,10 @@ __global__ __launch_bounds__(kScatThreads) void schedule_scatter_sec_kernel(cons
 // profiles/r03/cmp_coop_order_p7_65536.txt.)
 //
 // The same single launch with an ordinary launch and a software grid barrier, for at most
-// kOneLaunchChunks workgroups of kScatThreads threads: that many fit the chip at once (one per CU at
-// most, a quarter of its wave slots; the decoder's stream runs nothing beside them), so every
-// workgroup of the grid is resident and the barrier cannot wait on one that was never scheduled.
+// kOneLaunchChunks workgroups of kScatThreads threads, and never more than the device holds at once
+// (one_launch_capacity: occupancy per CU x CUs; the decoder's stream runs nothing beside them), so
+// every workgroup of the grid is resident and the barrier cannot wait on one that was never scheduled;
+// a larger grid takes the two-launch form.
 // bar[0] counts arrivals; bar[1] departures, and the last workgroup to leave zeroes both for the next
 // launch (bar comes zeroed from qec_decoder_create; graph replays reuse it the same way).
 // Measured slower than the two launches it replaces (P7 65 536: 0.082 vs 0.070 ms per decode call,
@@ -411,6 +413,28 @@ __global__ __launch_bounds__(kScatThreads) void schedule_one_launch_kernel(const
     grid_arrive_wait(bar, (uint32_t)nch);
     scatter_fused_body(key, B, chunk, nch, nbk, counts, perm, s, blockIdx.x);
     grid_depart(bar, (uint32_t)nch);
+}
+
+// Workgroups of schedule_one_launch_kernel<MODE> the current device holds at once (occupancy per CU x
+// CUs), cached per device: the software grid barrier is safe only when every workgroup of the grid is
+// resident, which a smaller device or partition (fewer CUs) may not give kOneLaunchChunks.
+template <int MODE>
+static int one_launch_capacity()
+{
+    static std::atomic<int> cached[64] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+    int cap = cached[dev].load(std::memory_order_relaxed);  // every writer stores the same value
+    if (cap == 0) {
+        int per_cu = 0, cus = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, schedule_one_launch_kernel<MODE>, kScatThreads, 0) !=
+                hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            per_cu = cus = 0;
+        cap = per_cu > 0 && cus > 0 ? per_cu * cus : -1;  // -1: unknown, never take the one-launch form
+        cached[dev].store(cap, std::memory_order_relaxed);
+    }
+    return cap;
 }
 
 // The whole order pass in one launch, for small batches (where the passes above are mostly launch
@@ -587,7 +611,11 @@ int launch_schedule(const uint8_t* sX, const uint8_t* sZ, bool sbits, long long 
         *sectors_out = true;
         return QEC_OK;
     }
-    if (method == QEC_ORDER_ONE_LAUNCH && fused && bar != nullptr && nch <= kOneLaunchChunks) {
+    const int one_cap = method != QEC_ORDER_ONE_LAUNCH ? 0
+                        : sbits                       ? one_launch_capacity<2>()
+                        : shortrows                   ? one_launch_capacity<1>()
+                                                      : one_launch_capacity<0>();
+    if (method == QEC_ORDER_ONE_LAUNCH && fused && bar != nullptr && nch <= kOneLaunchChunks && nch <= one_cap) {
         // histogram, grid barrier, offsets and scatter in one launch (schedule_one_launch_kernel)
         if (sbits)
             hipLaunchKernelGGL(schedule_one_launch_kernel<2>, dim3(nch), dim3(kScatThreads), 0, st, sX, sZ, B,

@@ -41,3 +41,15 @@ def shard_range(total, rank, world):
     base, rem = divmod(total, world)
     lo = rank * base + min(rank, rem)
     return lo, lo + base + (1 if rank < rem else 0)
+
+
+def bit_rows(s):
+    """[B, m] 0/1 syndrome bytes (torch tensor) -> [B, ceil(m / 32)] int32 bit rows, bit c % 32 of
+    word c / 32 = check c: the layout of qec_decode_bits_packed_dev and the Monte-Carlo pipeline."""
+    import torch
+    B, m = s.shape
+    w = -(-m // 32)
+    pad = torch.zeros((B, 32 * w), dtype=torch.int64, device=s.device)
+    pad[:, :m] = (s != 0).to(torch.int64)
+    v = (pad.view(B, w, 32) << torch.arange(32, device=s.device, dtype=torch.int64)).sum(2)
+    return torch.where(v >= 2 ** 31, v - 2 ** 32, v).to(torch.int32).contiguous()

@@ -54,6 +54,19 @@ def test_bench_two_ranks():
     assert 0 < b["executed_iteration_fraction"] <= 1
 
 
+def test_bench_plain_python_two_gpus():
+    """`python bench.py --gpus 2` with no launcher starts the two ranks itself (a child
+    torch.distributed.run) and reports them: never a one-GPU line labelled --gpus 2."""
+    lines = run([sys.executable, "bench.py", "--gpus", "2", "--global-batch", "16384", "--no-cpu", "--no-extras",
+                 "--steps", "3", "--warmup", "1"], {})
+    assert len(lines) == 1, lines
+    b = lines[0]
+    assert b["n_gpus"] == 2 and b["config"]["parallelism"] == "dp2" and b["config"]["per_gpu_batch"] == 8192
+    g = b["gather"]
+    assert "error" not in g, g
+    assert g["world_size"] == 2 and g["rank0_shard_intact"] is True
+
+
 def test_psweep_two_ranks_equal_one():
     args = ["--total", "16384", "--ps", "0.01", "0.05", "--reps", "1", "--batch", "8192"]
     two = run(launch(2, "tools/psweep.py", *args), {})

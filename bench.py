@@ -18,6 +18,8 @@ Prints one JSON line (rank 0).  Extra objects:
                   SQ_INSTS_VALU per launch (rocprofv3 PMC, profiles/pmc_<code>.json, per syndrome
                   x the batch) x 2 cycles / (1024 SIMDs x 2.4 GHz x launch time), launch time
                   from HIP events on the launch stream in this run; traffic = PMC HBM bytes.
+                  frac is the counter-exact figure; cost-weighted figures, the LDS issue fraction and
+                  the LDS bank-conflict share sit beside it (LDS is a co-bound of the P61 kernels).
   roofline_hbm_alg  SURVEY.md 8(d)'s HBM-resident flooding-schedule bytes over the launch time:
                   valid only if frac <= 1 (the engine keeps messages in VGPRs and takes exact
                   shortcuts, so it does far less than that schedule's traffic).
@@ -148,6 +150,9 @@ def main():
     ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
                     help="decoder option for the timed run (qec_decoder_set_option), e.g. schedule=0")
     ap.add_argument("--no-gather", action="store_true", help="N > 1: skip the RCCL gather measurements")
+    ap.add_argument("--graph", action="store_true",
+                    help="time the step as a replay of one captured HIP graph of it (same kernels, no per-launch "
+                         "host work or inter-launch gaps); without it the replay is reported in `graph`")
     ap.add_argument("--no-extras", action="store_true",
                     help="only the timed steps (profiling runs: no full-arithmetic / phase / sustained re-timings)")
     args = ap.parse_args()
@@ -205,6 +210,7 @@ def main():
     sZ = torch.empty((B, code.numEqsZ), dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream(dev)
     dec.sample_syndrome_dev(SEED, lo, p, sX, sZ, stream=stream)
+    S = {"stream": stream}  # the step's launch stream (a capture stream while a graph is recorded)
     its = torch.empty((B, 2), dtype=torch.int32, device=dev)
     packed = args.output == "packed"
     bits = args.input == "bits"
@@ -216,10 +222,10 @@ def main():
         outs = (rec, its)
 
         def step_bytes():
-            dec.decode_batch_packed_dev(sX, sZ, p, iters, args.stop, rec, its, stream=stream)
+            dec.decode_batch_packed_dev(sX, sZ, p, iters, args.stop, rec, its, stream=S["stream"])
 
         def step_bits():
-            dec.decode_bits_packed_dev(sXb, sZb, p, iters, args.stop, rec, its, stream=stream)
+            dec.decode_bits_packed_dev(sXb, sZb, p, iters, args.stop, rec, its, stream=S["stream"])
 
         step = step_bits if bits else step_bytes
     else:
@@ -229,8 +235,11 @@ def main():
         outs = (eX, eZ, fl, its)
 
         def step():
-            dec.decode_batch_dev(sX, sZ, p, iters, args.stop, eX, eZ, fl, its, stream=stream)
+            dec.decode_batch_dev(sX, sZ, p, iters, args.stop, eX, eZ, fl, its, stream=S["stream"])
 
+    eager_step = step
+    if args.graph:
+        step = capture_graph(step, S, dev)
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
@@ -333,6 +342,12 @@ def main():
         out["sustained"] = sustained(step, stream, dev, world, ms_per_step, args.min_seconds,
                                      global_batch if scaling == "strong" else B * world)
 
+    if not args.no_extras and not args.graph:
+        out["graph"] = graph_retime(eager_step, S, dev, stream, B, outs, world, global_batch if scaling == "strong"
+                                    else B * world, steps)
+    if args.graph:
+        out["config"]["launch"] = "hip graph replay"
+
     if world > 1 and not args.no_gather and packed:
         try:
             out["gather"] = gather_measure(dec, step, rec, B, world, rank, dev, stream, steps, global_batch, backend)
@@ -348,6 +363,48 @@ def main():
         dist.destroy_process_group()
     if rank == 0:
         print(json.dumps(out), flush=True)
+
+
+def capture_graph(step, S, dev):
+    """One step captured into a HIP graph (torch.cuda.CUDAGraph: hipStreamBeginCapture on a side stream;
+    the decoder's device entry points are capture-safe and allocate nothing at max_batch); returns its
+    replay on the current stream."""
+    import torch
+    cap = torch.cuda.Stream(dev)
+    cap.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(cap):  # one eager step on the side stream first (workspace already sized)
+        S["stream"] = cap
+        step()
+    torch.cuda.current_stream(dev).wait_stream(cap)
+    torch.cuda.synchronize(dev)
+    g = torch.cuda.CUDAGraph()
+    try:
+        with torch.cuda.graph(g, stream=cap):
+            step()
+    finally:
+        S["stream"] = torch.cuda.current_stream(dev)
+    torch.cuda.synchronize(dev)
+    return g.replay
+
+
+def graph_retime(step, S, dev, stream, B, outs, world, per_step_units, steps):
+    """The same step replayed from one captured HIP graph: K replays between synchronisations (max over
+    ranks), outputs compared with the eager step's."""
+    import torch
+    ref = [t.clone() for t in outs]
+    try:
+        replay = capture_graph(step, S, dev)
+    except Exception as exc:  # noqa: BLE001 -- reported, the eager line stands
+        return {"error": "%s: %s" % (type(exc).__name__, exc)}
+    for t in outs:
+        t.zero_()
+    replay()
+    torch.cuda.synchronize(dev)
+    same = all(torch.equal(r, t) for r, t in zip(ref, outs))
+    elapsed, kernel_ms = timed_steps(replay, steps, stream, dev, world)
+    return {"what": "the timed step replayed from one captured HIP graph", "steps": steps,
+            "ms_per_step": round(elapsed / steps * 1e3, 4), "syndromes_per_s": round(per_step_units * steps / elapsed, 1),
+            "kernel_ms": round(kernel_ms, 4), "identical": bool(same)}
 
 
 def relaunch(nproc):
@@ -409,16 +466,20 @@ def valu_roofline(pm, path, B, kernel_ms):
                  "profile": os.path.relpath(path, ROOT), "profile_batch": pm.get("batch"),
                  "profile_frac": pm.get("valu_issue_frac")})
     if pm.get("valu_weighted_slots_per_syndrome"):
-        # cost-weighted: a v_rcp_f32 (transcendental, quarter rate: 8.1 vs 2.1-2.4 cycles for v_mul /
-        # v_fma in profiles/r03/valu_probe.json) takes four issue slots; this is the headline frac
-        slots = pm["valu_weighted_slots_per_syndrome"] * B
-        wach = slots / (kernel_ms * 1e-3) / 1e12
-        base.update({"achieved": round(wach, 4), "frac": round(wach / peak, 4), "frac_unweighted": round(ach / peak, 4),
-                     "weighting": "VALU issue slots, SQ_INSTS_VALU_TRANS_F32 counted 4x (probe: v_rcp_f32 8.1 "
-                                  "cycles vs 2.1-2.4 for v_mul/v_add/v_fma at full occupancy)",
-                     "valu_trans_per_launch": int(round(pm["valu_trans_per_launch"] * B / pm["batch"]))})
+        # secondary: cost-weighted issue, a transcendental (v_rcp_f32, SQ_INSTS_VALU_TRANS_F32) priced at
+        # 4 slots (this repo's probe: 8.1 vs 2.1-2.4 cycles at full occupancy) and at 2 slots
+        # (MI355X_MICROARCH.md's issue-cost row: 8 vs 4 cycles for one wave)
+        trans = pm["valu_trans_per_launch"] * B / pm["batch"]
+        for label, w in (("frac_weighted_probe4x", 4), ("frac_weighted_guide2x", 2)):
+            wach = (insts + (w - 1) * trans) / (kernel_ms * 1e-3) / 1e12
+            base[label] = round(wach / peak, 4)
+        base["weighting"] = ("frac is the counter-exact SQ_INSTS_VALU issue; the weighted figures count each "
+                             "SQ_INSTS_VALU_TRANS_F32 as 4 (probe) or 2 (guide) issue slots")
+        base["valu_trans_per_launch"] = int(round(trans))
     if pm.get("lds_issue_frac") is not None and pm.get("kernel_trace_avg_ns"):
         base["lds_issue_frac"] = round(pm["lds_issue_frac"] * pm["kernel_trace_avg_ns"] * 1e-6 / kernel_ms, 4)
+    if pm.get("lds_bank_conflict_share") is not None:
+        base["lds_bank_conflict_share"] = pm["lds_bank_conflict_share"]
     return base
 
 

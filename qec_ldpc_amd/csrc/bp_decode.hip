@@ -108,6 +108,11 @@ namespace qec {
 #ifndef QEC_ZERO_SYNDROME
 #define QEC_ZERO_SYNDROME 1
 #endif
+//   QEC_ZERO_OUTCOME fixed / reference stop: a wave whose sector syndromes are all zero takes the launch's
+//                    precomputed zero-syndrome outcome (zero_outcome) instead of iterating
+#ifndef QEC_ZERO_OUTCOME
+#define QEC_ZERO_OUTCOME 1
+#endif
 //   QEC_SYN_EARLY    syndrome stop: iteration 0 tests the syndrome before forming its messages
 #ifndef QEC_SYN_EARLY
 #define QEC_SYN_EARLY 1
@@ -144,6 +149,11 @@ namespace qec {
 #ifndef QEC_SYN_RELAUNDER
 #define QEC_SYN_RELAUNDER 1
 #endif
+//   QEC_SYN_SKIP_SEEN  syndrome stop: an iteration whose hard decision equals (group-wide) one of the two
+//                      last tested ones -- both failed, or the group would have stopped -- skips the test
+#ifndef QEC_SYN_SKIP_SEEN
+#define QEC_SYN_SKIP_SEEN 1
+#endif
 //   QEC_SCALED_DIV   var passes with at most 4 factors per fold divide guard-free on 2^32-scaled folds
 #ifndef QEC_SCALED_DIV
 #define QEC_SCALED_DIV 1
@@ -179,6 +189,11 @@ namespace qec {
 #define QEC_COL_GROUP 0
 #endif
 #define QEC_PICK(macro, dflt) ((macro) >= 0 ? (macro) != 0 : (dflt))
+//   QEC_LIST_STAMPS  experiment builds only: syndrome-stop sectors add s_memtime phase spans (cycles) and
+//                    counts to g_list_stamps (read by qec_debug_list_stamps, tools/kbench/list_stamps.py)
+#ifndef QEC_LIST_STAMPS
+#define QEC_LIST_STAMPS 0
+#endif
 
 // Per-variant tuning: minimum waves per SIMD for the register allocator, and the options above.
 //   QEC_SEQ_MINW_X / _Z  experiment: min waves per SIMD of the sector-launch kernels (MODE 3 / 4), all variants
@@ -209,6 +224,33 @@ struct Tune {
     static constexpr bool kFastDiv = QEC_PICK(QEC_FASTDIV, FASTDIV_);
     static constexpr bool kSaturate = QEC_PICK(QEC_SATURATE, SATURATE_);
     static constexpr bool kAgreeSyn = false;  // the syndrome stop takes the agreement test (kAgree)
+    static constexpr int kSeqSynWavesX = kMinWavesSyn, kSeqSynWavesZ = kMinWavesSyn;  // sector launches, syndrome stop
+};
+
+//   QEC_SEQ_AGREE_SYN        the syndrome-stop sector launches (MODE 3 / 4) take the agreement test and the
+//                            cycle jump (SeqSynTune), at their own occupancy (QEC_SEQ_SYN_MINW_X / _Z)
+#ifndef QEC_SEQ_AGREE_SYN
+#define QEC_SEQ_AGREE_SYN 0
+#endif
+#ifndef QEC_SEQ_SYN_MINW_X
+#define QEC_SEQ_SYN_MINW_X 5
+#endif
+#ifndef QEC_SEQ_SYN_MINW_Z
+#define QEC_SEQ_SYN_MINW_Z 0
+#endif
+//   QEC_SEQ_SYN_MINREG       the P61 syndrome-stop sector launches from the minreg unit (bp_decode_p61.hip)
+#ifndef QEC_SEQ_SYN_MINREG
+#define QEC_SEQ_SYN_MINREG 0
+#endif
+// The syndrome-stop sector launches of a variant: with the agreement test a sector that never satisfies
+// its syndrome jumps to its cap once its hard state cycles, instead of running every hard iteration (the
+// one-wave-per-syndrome kernels leave the test out to stay spill-free; a kernel compiled for one sector
+// has the registers for it at three waves per SIMD).
+template <class TU>
+struct SeqSynTune : TU {
+    static constexpr bool kAgreeSyn = QEC_SEQ_AGREE_SYN != 0;
+    static constexpr int kSeqSynWavesX = QEC_SEQ_SYN_MINW_X > 0 ? QEC_SEQ_SYN_MINW_X : TU::kMinWavesSyn;
+    static constexpr int kSeqSynWavesZ = QEC_SEQ_SYN_MINW_Z > 0 ? QEC_SEQ_SYN_MINW_Z : TU::kMinWavesSyn;
 };
 
 //   QEC_LIST_MINW_P61 / _P7   min waves per SIMD of the list-mode kernels (ListTune); QEC_LIST_AGREE 0: no
@@ -225,11 +267,29 @@ struct Tune {
 #ifndef QEC_LIST_MERGE_ONLY
 #define QEC_LIST_MERGE_ONLY 1
 #endif
-// The list-mode (MODE 2) tuning of a variant: its own occupancy and the agreement test with the cycle
-// jump under the syndrome stop (see kAgree).
-template <class TU, int LW>
+//   QEC_LIST_SECTORS       list mode as two launches, one kernel per sector (MODE 5 / 6), each compiled
+//                          (and its registers allocated) for its own sector, instead of one kernel for both
+//   QEC_LIST_GO            list mode skips iteration 0's syndrome test (the triage listed the sector because it fails)
+#ifndef QEC_LIST_GO
+#define QEC_LIST_GO 1
+#endif
+#ifndef QEC_LIST_SECTORS
+#define QEC_LIST_SECTORS 0
+#endif
+//   QEC_LIST_MINW_X / _Z   experiment: min waves per SIMD of the per-sector list kernels (all variants)
+#ifndef QEC_LIST_MINW_X
+#define QEC_LIST_MINW_X 0
+#endif
+#ifndef QEC_LIST_MINW_Z
+#define QEC_LIST_MINW_Z 0
+#endif
+// The list-mode (MODE 2, or per sector MODE 5 / 6) tuning of a variant: its own occupancies and the
+// agreement test with the cycle jump under the syndrome stop (see kAgree).
+template <class TU, int LW, int LWX = 0, int LWZ = 0>
 struct ListTune : TU {
     static constexpr int kMinWavesSyn = LW;
+    static constexpr int kListMinWavesX = QEC_LIST_MINW_X > 0 ? QEC_LIST_MINW_X : LWX > 0 ? LWX : LW;
+    static constexpr int kListMinWavesZ = QEC_LIST_MINW_Z > 0 ? QEC_LIST_MINW_Z : LWZ > 0 ? LWZ : LW;
     static constexpr bool kAgreeSyn = QEC_LIST_AGREE != 0;
 };
 
@@ -303,6 +363,9 @@ struct BpArgs {
     // iteration-0 tables of both sectors computed on the host (QEC_TABLE0_HOST: the same operations,
     // so the same bits, as table0_entry on the device; each workgroup copies them to LDS)
     float tab0[kMaxTab0];
+    // zero-syndrome outcome of each sector under the fixed / reference stop (zero_outcome; 0: none):
+    // kZsValid | decision bit | conv-fail << 1 | syndrome-fail << 2 | iterations << 8
+    uint32_t zs[2];
     int SX[kMaxRL], SZ[kMaxRL];  // rotation of block (r, l) between check and variable views
     int DX[kMaxR], DZ[kMaxR];    // check-view lane lambda holds check (r, (lambda + D[r]) mod P)
     int CX[kMaxL], CZ[kMaxL];    // var-view lane mu holds variable (l, (mu + C[l]) mod P)
@@ -399,6 +462,33 @@ struct GeneratedShifts {
     __device__ static constexpr int coloff(const BpArgs&, int l) { return SEC ? tabs.CZ[l] : tabs.CX[l]; }
 };
 
+// ---- experiment stamps (QEC_LIST_STAMPS) ------------------------------------
+#if QEC_LIST_STAMPS
+// [0..7] summed phase spans, [8..15] counts: added up per workgroup in LDS (one wave per workgroup:
+// lane 0's plain adds), flushed to g_list_stamps once per workgroup at the kernel's end
+static __device__ unsigned long long g_list_stamps[16];
+__device__ __forceinline__ unsigned long long* stamp_lds()
+{
+    __shared__ unsigned long long s[16];
+    return s;
+}
+__device__ __forceinline__ unsigned long long stamp_now()
+{
+    unsigned long long t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+}
+__device__ __forceinline__ void stamp_add(int k, unsigned long long dt, unsigned long long n = 1)
+{
+    if (__lane_id() == 0) {
+        stamp_lds()[k] += dt;
+        stamp_lds()[8 + k] += n;
+    }
+}
+#endif
+
 // ---- lane helpers ----------------------------------------------------------
 __device__ __forceinline__ float bperm(int addr, float v)
 {
@@ -491,7 +581,7 @@ __device__ __forceinline__ bool group_all_sh(bool pred, const Lane& ln, int P)
     }
 }
 
-__device__ __forceinline__ bool outside(float x) { return !(x > 0.01f && x < 0.99f); }
+__host__ __device__ __forceinline__ bool outside(float x) { return !(x > 0.01f && x < 0.99f); }
 // AND of two wave-uniform (scalar) conditions without a short-circuit branch
 __device__ __forceinline__ bool band(bool a, bool b) { return (int)a & (int)b; }
 
@@ -993,6 +1083,10 @@ constexpr bool kAgree()
     return QEC_AGREE && (STOP != QEC_STOP_SYNDROME || QEC_AGREE_SYN || TU::kAgreeSyn);
 }
 
+// QEC_SYN_SKIP_SEEN for L columns (the never-seen marker ~0u is no decision mask when L < 32)
+template <int L>
+constexpr bool kSkipSeen() { return QEC_SYN_SKIP_SEEN && L < 32; }
+
 // One BP iteration; returns true if this group stops after it.
 // hard: every variable->check message of this sector is exactly +0 or 1.0 (wave-uniform).
 // agreed: set when the iteration took the agreement path (hard sector, every variable's inputs
@@ -1002,7 +1096,7 @@ constexpr bool kAgree()
 template <int R, int L, int SEC, int STOP, bool LAST, class SH, class TU>
 __device__ __forceinline__ bool iteration(const BpArgs& a, float (&msg)[R][L], uint32_t sbits, int n, Lane& ln,
                                           float pp, float one_minus_pp, bool& hard, bool& agreed, bool& vagree,
-                                          uint32_t& hd_out)
+                                          uint32_t& hd_out, uint32_t (&seen)[2])
 {
     const int P = SH::P(a);
     // launder the permute bases so their per-rotation selects are recomputed inside the
@@ -1043,10 +1137,31 @@ __device__ __forceinline__ bool iteration(const BpArgs& a, float (&msg)[R][L], u
         if (n % 10 == 0) return group_all_sh<SH>(lane_converged<R, L>(msg), ln, P);  // DecoderCPU.h:287-290
     } else if constexpr (STOP == QEC_STOP_SYNDROME) {
         hd_out = hdmask;  // the hard decision of the new state (what the post-processing would compute)
+        // The test is a function of the group's hard decisions (and its fixed syndrome): if they equal,
+        // group-wide, one of the last two tested decisions, it fails again -- an active group has failed
+        // every test so far.  Skipped then (sectors that never satisfy their syndrome mostly repeat one
+        // decision or alternate between two).  seen[] holds whole-group tested states: it is updated
+        // group-uniformly (kept when the decision is seen[0], else pushed).
+        const bool same0 = kSkipSeen<L>() && group_all_sh<SH>(hdmask == seen[0], ln, P);
+        if constexpr (kSkipSeen<L>()) {
+            const bool same1 = group_all_sh<SH>(hdmask == seen[1], ln, P);
+            if (all_live_sh<SH>(same0 || same1, ln.live)) {
+                if (!same0) {
+                    seen[1] = seen[0];
+                    seen[0] = hdmask;
+                }
+                return false;
+            }
+        }
         // launder the bases again: the test's rotations are var_pass's return rotations, whose
         // addresses would otherwise be kept live across the whole var pass for reuse here
         if constexpr (SH::kMaskSelect && QEC_SYN_RELAUNDER) asm volatile("" : "+v"(ln.b0), "+v"(ln.b1));
-        return group_all_sh<SH>(lane_syndrome_ok<R, L, SEC, SH>(a, hdmask, sbits, ln), ln, P);
+        const bool stop = group_all_sh<SH>(lane_syndrome_ok<R, L, SEC, SH>(a, hdmask, sbits, ln), ln, P);
+        if (kSkipSeen<L>() && !same0) {
+            seen[1] = seen[0];
+            seen[0] = hdmask;
+        }
+        return stop;
     }
     return false;
 }
@@ -1105,14 +1220,16 @@ __device__ __forceinline__ void pattern_masks(const float* __restrict__ tab, uns
     cvpat = __ballot(li < (1 << R) && cp);
 }
 
-template <int R, int L, int SEC, int STOP, class SH>
+// GO (list mode): the sector is known to go on past iteration 0 -- the triage listed it because its
+// iteration-0 hard decision fails the syndrome (triage.hip) -- so only the messages are formed.
+template <int R, int L, int SEC, int STOP, class SH, bool GO = false>
 __device__ __forceinline__ bool iteration0(const BpArgs& a, float (&msg)[R][L], uint32_t sbits, const Lane& ln,
                                            const float* __restrict__ tab, uint32_t& hd_out, bool& cv_out,
                                            bool& msg_out, unsigned long long hdpat, unsigned long long cvpat)
 {
     const int P = SH::P(a);
     const int* et = SH::template table<SEC>(a);
-    constexpr bool HD = STOP == QEC_STOP_SYNDROME;
+    constexpr bool HD = STOP == QEC_STOP_SYNDROME && !GO;
     msg_out = true;
     if constexpr (HD && QEC_SYN_EARLY && L * R <= 64) {
         // Syndrome stop: a variable's hard decision after this iteration, and whether its R
@@ -1175,11 +1292,56 @@ __device__ __forceinline__ bool iteration0(const BpArgs& a, float (&msg)[R][L], 
     }
     if constexpr (STOP == QEC_STOP_REF) {
         return group_all_sh<SH>(lane_converged<R, L>(msg), ln, P);  // n = 0: DecoderCPU.h:287-290
-    } else if constexpr (STOP == QEC_STOP_SYNDROME) {
+    } else if constexpr (STOP == QEC_STOP_SYNDROME && !GO) {
         hd_out = hdmask;
         return group_all_sh<SH>(lane_syndrome_ok<R, L, SEC, SH>(a, hdmask, sbits, ln), ln, P);
     }
     return false;
+}
+
+// ---- zero syndrome under the fixed / reference stop ----------------------------------
+// A sector whose syndrome is zero keeps every edge's message equal to every other's in every iteration:
+// every check sees L equal inputs and syndrome 0, every variable R equal inputs, and each update's
+// output depends only on those.  So its decode is a scalar recursion, evaluated on the host with the very
+// operations of check_pass / var_pass on equal inputs (same IEEE fp32 operations, -ffp-contract=off:
+// every leave-one-out product is a left fold of L - 1 equal factors whatever its prefix reuse; the
+// numerators and denominators left folds of R - 1, or R in the last iteration, equal factors; the
+// division correctly rounded; the hard forms and cycle jump are bit-identical to it).  The outcome --
+// decision (every variable the same), convergence and syndrome flags, iteration count -- is the same
+// for every zero-syndrome sector of the launch, which then skips its iterations (decode_sector).
+constexpr uint32_t kZsValid = 1u << 31;
+template <int R, int L>
+uint32_t zero_outcome(float pp, int N, int stop)
+{
+    if (!(pp > 0.0f && pp < 1.0f) || N < 2 || N > 0xFFFF || stop == QEC_STOP_SYNDROME || QEC_PHASE_STATS || !QEC_TABLE0)
+        return 0u;
+    float q = table0_entry<R, L>(pp, 0);  // iteration 0 (syndrome pattern 0), as iteration0
+    int it = 1;
+    const float one_minus_pp = 1.0f - pp;
+    if (!(stop == QEC_STOP_REF && outside(q))) {  // DecoderCPU.h:287-290 at n = 0
+        for (int n = 1; n < N; ++n) {
+            const float a = __builtin_fmaf(-2.0f, q, 1.0f);
+            float t = 1.0f;
+            if (L >= 2) {
+                t = a;
+                for (int k = 2; k < L; ++k) t = t * a;
+            }
+            const float g = __builtin_fmaf(-0.5f, t, 0.5f);  // syndrome 0: h = -1/2
+            const float b = 1.0f - g;
+            const int F = n == N - 1 ? R : R - 1;  // the last iteration includes the self message
+            float P0 = one_minus_pp, P1 = pp;
+            for (int k = 0; k < F; ++k) {
+                P0 = P0 * b;
+                P1 = P1 * g;
+            }
+            q = P1 / (P0 + P1);
+            ++it;
+            if (stop == QEC_STOP_REF && n % 10 == 0 && outside(q)) break;
+        }
+    }
+    const bool d = q >= 0.5f;
+    const bool syn_fail = d && (L & 1);  // every check holds L equal decisions, syndrome 0
+    return kZsValid | (uint32_t)d | (uint32_t)!outside(q) << 1 | (uint32_t)syn_fail << 2 | (uint32_t)it << 8;
 }
 
 // ---- cycle jump --------------------------------------------------------------
@@ -1290,7 +1452,8 @@ __device__ __forceinline__ void emit_decisions(const BpArgs& a, const Lane& ln, 
     wave_sync();  // the next sector reuses the stage
 }
 
-template <int R, int L, int SEC, int STOP, class SH, class TU>
+// GO: list mode (the sector is known to go on past iteration 0, see iteration0)
+template <int R, int L, int SEC, int STOP, class SH, class TU, bool GO = false>
 __device__ __forceinline__ void decode_sector(const BpArgs& a, Lane& ln, uint32_t b, bool in_range, float pp,
                                               uint32_t sbits, const float* __restrict__ tab0, uint32_t& flags,
                                               int& iters_out, uint8_t* __restrict__ stage)
@@ -1303,7 +1466,7 @@ __device__ __forceinline__ void decode_sector(const BpArgs& a, Lane& ln, uint32_
     // hard decision is 0 when every tab0[r] < 0.5, its syndrome is the input's (0), and the sector
     // stops after that iteration with e = 0, conv = every tab0[r] outside (0.01, 0.99).  The same
     // outputs without the iteration's rotations (not when the final messages are requested).
-    if constexpr (STOP == QEC_STOP_SYNDROME && QEC_TABLE0 && QEC_ZERO_SYNDROME) {
+    if constexpr (STOP == QEC_STOP_SYNDROME && QEC_TABLE0 && QEC_ZERO_SYNDROME && !GO) {
         if (a.maxIter >= 2 && a.q == nullptr && all_live(sbits == 0u, in_range)) {
             bool low = true, cv = true;
 #pragma unroll
@@ -1320,6 +1483,20 @@ __device__ __forceinline__ void decode_sector(const BpArgs& a, Lane& ln, uint32_
         }
     }
 
+#if QEC_LIST_STAMPS
+    const unsigned long long ts0 = stamp_now();
+#endif
+    // Zero syndrome under the fixed / reference stop: the launch's precomputed outcome (zero_outcome)
+    if constexpr (STOP != QEC_STOP_SYNDROME) {
+        const uint32_t zs = a.zs[SEC];
+        if (zs != 0u && a.q == nullptr && all_live(sbits == 0u, in_range)) {
+            emit_decisions<L, SEC, SH>(a, ln, b, in_range, (zs & 1u) ? (uint32_t)((1ull << L) - 1ull) : 0u, stage);
+            if (zs & 2u) flags |= SEC ? QEC_CONVERGENCE_FAIL_Z : QEC_CONVERGENCE_FAIL_X;
+            if (zs & 4u) flags |= SEC ? QEC_SYNDROME_FAIL_Z : QEC_SYNDROME_FAIL_X;
+            iters_out = (int)((zs >> 8) & 0xFFFFu);
+            return;
+        }
+    }
     // InitVarNodes: every edge starts at p' (DecoderCPU.h:135-148, 265-267)
     float msg[R][L];
 #pragma unroll
@@ -1346,19 +1523,24 @@ __device__ __forceinline__ void decode_sector(const BpArgs& a, Lane& ln, uint32_
     // syndrome test the same test, so they are reused (group-uniform).
     uint32_t hd_last = 0;
     bool syn_last = false, hd_valid = false;
+    uint32_t seen[2] = {~0u, ~0u};  // the group's last two tested (failed) hard decisions (QEC_SYN_SKIP_SEEN)
     // iteration 0 of the syndrome stop may leave the messages unformed (every group stopped there):
     // then cv0 is each lane's convergence test of them (iteration0)
     bool cv0 = true, msg_built = true;
     unsigned long long hdpat = 0, cvpat = 0;
-    if constexpr (STOP == QEC_STOP_SYNDROME && QEC_SYN_EARLY && QEC_TABLE0) pattern_masks<R>(tab0, hdpat, cvpat);
+    if constexpr (STOP == QEC_STOP_SYNDROME && QEC_SYN_EARLY && QEC_TABLE0 && !GO) pattern_masks<R>(tab0, hdpat, cvpat);
     if (QEC_TABLE0 && N >= 2 && active) {  // iteration 0 by table (see iteration0)
         ++it;
-        syn_last = iteration0<R, L, SEC, STOP, SH>(a, msg, sbits, ln, tab0, hd_last, cv0, msg_built, hdpat, cvpat);
+        syn_last = iteration0<R, L, SEC, STOP, SH, GO>(a, msg, sbits, ln, tab0, hd_last, cv0, msg_built, hdpat, cvpat);
         hd_valid = true;
+        if (STOP == QEC_STOP_SYNDROME && !GO) seen[0] = hd_last;  // tested (a group going on failed it)
         if (syn_last) active = false;
         if constexpr (QEC_PHASE_STATS) ph_soft += 1;
         n = 1;
     }
+#if QEC_LIST_STAMPS
+    const unsigned long long ts1 = stamp_now();
+#endif
     // iterations n .. N-2 (DecoderCPU.h:280-291); the last one is peeled below
     for (; n < N - 1; ++n) {
         if (!__any(active)) break;  // DecoderCPU.h:282 (fixed: only after a cycle jump)
@@ -1369,7 +1551,7 @@ __device__ __forceinline__ void decode_sector(const BpArgs& a, Lane& ln, uint32_
             ++it;
             const bool was_hard = hard;
             syn_last = iteration<R, L, SEC, STOP, false, SH, TU>(a, msg, sbits, n, ln, pp, one_minus_pp, hard, agreed,
-                                                                 vagree, hd_last);
+                                                                 vagree, hd_last, seen);
             hd_valid = true;
             if (syn_last) active = false;
             if constexpr (QEC_PHASE_STATS) { ph_soft += !was_hard; ph_hard += was_hard && !agreed; ph_agree += agreed; }
@@ -1394,7 +1576,7 @@ __device__ __forceinline__ void decode_sector(const BpArgs& a, Lane& ln, uint32_
         ++it;
         const bool was_hard = hard;
         syn_last = iteration<R, L, SEC, STOP, true, SH, TU>(a, msg, sbits, n, ln, pp, one_minus_pp, hard, agreed, vagree,
-                                                            hd_last);
+                                                            hd_last, seen);
         hd_valid = true;
         if constexpr (QEC_PHASE_STATS) { ph_soft += !was_hard; ph_hard += was_hard && !agreed; ph_agree += agreed; }
         st_agreed = vagree;
@@ -1404,6 +1586,9 @@ __device__ __forceinline__ void decode_sector(const BpArgs& a, Lane& ln, uint32_
         iters_out = it + (int)__float_as_uint(msg[0][0]);
         return;
     }
+#if QEC_LIST_STAMPS
+    const unsigned long long ts2 = stamp_now();
+#endif
     // ---- post-processing of Decode (DecoderCPU.h:354-384) ----
     asm volatile("" : "+v"(sbits));  // its per-row bits are recomputed here, not held since the sector began
     const int* et = SH::template table<SEC>(a);
@@ -1448,7 +1633,19 @@ __device__ __forceinline__ void decode_sector(const BpArgs& a, Lane& ln, uint32_
         }
         syn_ok = group_all_sh<SH>(lane_syndrome_ok<R, L, SEC, SH>(a, hdmask, sbits, ln), ln, P);
     }
+#if QEC_LIST_STAMPS
+    const unsigned long long ts3 = stamp_now();
+#endif
     emit_decisions<L, SEC, SH>(a, ln, b, in_range, hdmask, stage);
+#if QEC_LIST_STAMPS
+    const unsigned long long ts4 = stamp_now();
+    if (STOP == QEC_STOP_SYNDROME) {
+        stamp_add(4 * SEC + 0, ts1 - ts0);
+        stamp_add(4 * SEC + 1, ts2 - ts1, (unsigned long long)(it > 1 ? it - 1 : 0));
+        stamp_add(4 * SEC + 2, ts3 - ts2);
+        stamp_add(4 * SEC + 3, ts4 - ts3);
+    }
+#endif
 
     if (!syn_ok) flags |= SEC ? QEC_SYNDROME_FAIL_Z : QEC_SYNDROME_FAIL_X;
     if (!conv) flags |= SEC ? QEC_CONVERGENCE_FAIL_Z : QEC_CONVERGENCE_FAIL_X;
@@ -1496,7 +1693,7 @@ __device__ __forceinline__ void decode_group(const BpArgs& a, const float* __res
                                              uint32_t sbPre = 0u)
 {
     constexpr bool SPLIT = MODE != 0;
-    constexpr bool kHasX = MODE != 4, kHasZ = MODE != 3;
+    constexpr bool kHasX = MODE != 4 && MODE != 6, kHasZ = MODE != 3 && MODE != 5;
     constexpr int kTabX = (1 << RX) * RX;
     // p' = (2/3) p, as the reference writes it (DecoderCPU.h:259)
     const float pp = 2.0f / 3.0f * a.errorProbability;
@@ -1508,15 +1705,17 @@ __device__ __forceinline__ void decode_group(const BpArgs& a, const float* __res
 #define QEC_PREFETCH_Z 1
 #endif
     const bool runX = kHasX && doX, runZ = kHasZ && (!doX || !SPLIT);
+    // list mode: every listed sector goes on past iteration 0 (decode_sector's GO)
+    constexpr bool GO = QEC_LIST_GO && (MODE == 2 || MODE == 5 || MODE == 6);
     // both sectors' syndrome loads are issued up front: the Z load's latency hides behind X
     const uint32_t sbX = pre ? sbPre : runX ? load_sbits<RX, 0, SH>(a, ln, b, in_range) : 0u;
     uint32_t sbZ = pre ? sbPre : (QEC_PREFETCH_Z && runZ) ? load_sbits<RZ, 1, SH>(a, ln, b, in_range) : 0u;
     if constexpr (kHasX) {
-        if (runX) decode_sector<RX, L, 0, STOP, SH, TU>(a, ln, b, in_range, pp, sbX, tab0, flags, itX, stage);
+        if (runX) decode_sector<RX, L, 0, STOP, SH, TU, GO>(a, ln, b, in_range, pp, sbX, tab0, flags, itX, stage);
     }
     if constexpr (kHasZ) {
         if (!pre && !QEC_PREFETCH_Z && runZ) sbZ = load_sbits<RZ, 1, SH>(a, ln, b, in_range);
-        if (runZ) decode_sector<RZ, L, 1, STOP, SH, TU>(a, ln, b, in_range, pp, sbZ, tab0 + kTabX, flags, itZ, stage);
+        if (runZ) decode_sector<RZ, L, 1, STOP, SH, TU, GO>(a, ln, b, in_range, pp, sbZ, tab0 + kTabX, flags, itZ, stage);
     }
     if (in_range && lane_i<SH>(ln) == 0) {
         uint8_t* fdst = a.rec != nullptr ? a.rec + b * (long long)a.recBytes + 2 * a.nb : a.flags + b;
@@ -1526,7 +1725,7 @@ __device__ __forceinline__ void decode_group(const BpArgs& a, const float* __res
             a.merge[b] = flags;  // for the Z launch (a word per syndrome, not the record's byte: one line each)
         } else if constexpr (MODE == 4) {
             *fdst = (uint8_t)(a.merge[b] | flags);  // the X launch's flags (same stream, earlier launch)
-        } else if (MODE == 2 && a.mergeOnly) {
+        } else if ((MODE == 2 || MODE == 5 || MODE == 6) && a.mergeOnly) {
             // the fused Monte-Carlo pipeline reads the flags from the merge word itself
             // (mc_survivor_kernel): no returned value to wait for
             __hip_atomic_fetch_or(&a.merge[b], flags, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1549,20 +1748,24 @@ __device__ __forceinline__ void decode_group(const BpArgs& a, const float* __res
 // past the triage, listX [0, counts[0]) then listZ [0, counts[1]), G per wave, each wave looping over
 // them (the grid does not depend on the lists' device-side lengths); merged as in split mode;
 // 3 / 4 (sector launches): sector X, then in a second launch on the same stream sector Z, of group k
-// in wave k (decode_group).
+// in wave k (decode_group); 5 / 6 (list mode per sector): MODE 2 over listX alone / listZ alone, each
+// kernel compiled for its own sector.
 template <class TU, int STOP, int MODE>
 constexpr int min_waves()
 {
     if constexpr (QEC_MIN_WAVES_PER_EU > 0) return QEC_MIN_WAVES_PER_EU;
-    if constexpr (STOP != QEC_STOP_SYNDROME && MODE == 3) return TU::kMinWavesX;
-    if constexpr (STOP != QEC_STOP_SYNDROME && MODE == 4) return TU::kMinWavesZ;
+    if constexpr (MODE == 5) return TU::kListMinWavesX;
+    if constexpr (MODE == 6) return TU::kListMinWavesZ;
+    if constexpr (MODE == 3) return STOP != QEC_STOP_SYNDROME ? TU::kMinWavesX : TU::kSeqSynWavesX + QEC_SYN_MINW_DELTA;
+    if constexpr (MODE == 4) return STOP != QEC_STOP_SYNDROME ? TU::kMinWavesZ : TU::kSeqSynWavesZ + QEC_SYN_MINW_DELTA;
     return STOP == QEC_STOP_SYNDROME ? TU::kMinWavesSyn + QEC_SYN_MINW_DELTA : TU::kMinWaves;
 }
 template <int RX, int RZ, int L, int STOP, class SH, class TU, int MODE>
 __global__ __launch_bounds__(64 * waves_per_block<TU>(), (min_waves<TU, STOP, MODE>()))
 void bp_decode_kernel(const BpArgs a)
 {
-    constexpr bool SPLIT = MODE == 1 || MODE == 2;
+    constexpr bool LIST = MODE == 2 || MODE == 5 || MODE == 6;
+    constexpr bool SPLIT = MODE == 1 || LIST;
     const int lane = threadIdx.x & 63;
     const long long wave = (long long)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     const int P = SH::P(a);
@@ -1584,12 +1787,23 @@ void bp_decode_kernel(const BpArgs a)
         }
         __syncthreads();
     }
+#if QEC_LIST_STAMPS
+    if (threadIdx.x < 16) stamp_lds()[threadIdx.x] = 0;
+    __syncthreads();
+    struct Flush {
+        __device__ ~Flush()
+        {
+            __syncthreads();
+            if (threadIdx.x < 16 && stamp_lds()[threadIdx.x]) atomicAdd(&g_list_stamps[threadIdx.x], stamp_lds()[threadIdx.x]);
+        }
+    } flush_stamps;
+#endif
     // this wave's decision stage for packed records (emit_decisions)
     constexpr int kStage = stage_bytes_per_wave<L, SH>();
     __shared__ __attribute__((aligned(8))) uint8_t stage_all[waves_per_block<TU>() * kStage];
     uint8_t* stage = stage_all + (threadIdx.x >> 6) * kStage;
-    if constexpr (MODE == 2) {
-        const long long nX = a.counts[0], nZ = a.counts[a.countStride];
+    if constexpr (LIST) {
+        const long long nX = MODE == 6 ? 0 : a.counts[0], nZ = MODE == 5 ? 0 : a.counts[a.countStride];
         const long long wXn = (nX + G - 1) / G, wTot = wXn + (nZ + G - 1) / G;
         const long long nw = (long long)gridDim.x * (blockDim.x >> 6);
         if constexpr (!QEC_LIST_PREFETCH) {
@@ -1602,7 +1816,7 @@ void bp_decode_kernel(const BpArgs a)
                 // be hoisted out of this loop into live registers (they spilled at 3 waves per SIMD)
                 int il = i, gbl = gb;
                 asm volatile("" : "+v"(il), "+v"(gbl));
-                decode_group<RX, RZ, L, STOP, SH, TU, 2>(a, tab0, stage, il, gbl, b, in_range, doX);
+                decode_group<RX, RZ, L, STOP, SH, TU, MODE>(a, tab0, stage, il, gbl, b, in_range, doX);
             }
             return;
         }
@@ -1627,7 +1841,7 @@ void bp_decode_kernel(const BpArgs a)
             bool dX2, ir2;
             const uint32_t b2 = entry(vw + 2 * nw, dX2, ir2);
             const uint32_t sb1 = vw + nw < wTot ? bits(b1, dX1, ir1) : 0u;
-            decode_group<RX, RZ, L, STOP, SH, TU, 2>(a, tab0, stage, i, gb, b0, ir0, dX0, true, sb0);
+            decode_group<RX, RZ, L, STOP, SH, TU, MODE>(a, tab0, stage, i, gb, b0, ir0, dX0, true, sb0);
             b0 = b1; dX0 = dX1; ir0 = ir1; sb0 = sb1;
             b1 = b2; dX1 = dX2; ir1 = ir2;
         }
@@ -1705,6 +1919,7 @@ KernelFn p61_minreg_kernel(int stop, bool split);  // bp_decode_p61.hip
 KernelFn p61_minreg_seq_kernel(int stop, int sec); // bp_decode_p61.hip
 KernelFn p7_minreg_kernel(int stop, bool split);   // bp_decode_p61.hip
 KernelFn p7_minreg_list_kernel();                  // bp_decode_p61.hip
+KernelFn p7_minreg_list_sec_kernel(int sec);       // bp_decode_p61.hip
 
 KernelFn phase_kernel(int P, int stop);  // bp_decode_phase.hip
 
@@ -1732,6 +1947,11 @@ KernelFn p61_minreg_seq_kernel(int stop, int sec)
     if (stop == QEC_STOP_FIXED)
         return sec ? bp_decode_kernel<4, 5, 10, QEC_STOP_FIXED, ShiftsP61, TuneP61MinReg, 4>
                    : bp_decode_kernel<4, 5, 10, QEC_STOP_FIXED, ShiftsP61, TuneP61MinReg, 3>;
+#if QEC_SEQ_SYN_MINREG
+    if (stop == QEC_STOP_SYNDROME)
+        return sec ? bp_decode_kernel<4, 5, 10, QEC_STOP_SYNDROME, ShiftsP61, SeqSynTune<TuneP61MinReg>, 4>
+                   : bp_decode_kernel<4, 5, 10, QEC_STOP_SYNDROME, ShiftsP61, SeqSynTune<TuneP61MinReg>, 3>;
+#endif
     return nullptr;
 }
 KernelFn p7_minreg_kernel(int stop, bool split)
@@ -1742,6 +1962,11 @@ KernelFn p7_minreg_kernel(int stop, bool split)
     return nullptr;
 }
 KernelFn p7_minreg_list_kernel() { return bp_decode_kernel<3, 3, 6, QEC_STOP_SYNDROME, ShiftsP7, ListTuneP7, 2>; }
+KernelFn p7_minreg_list_sec_kernel(int sec)
+{
+    return sec ? bp_decode_kernel<3, 3, 6, QEC_STOP_SYNDROME, ShiftsP7, ListTuneP7, 6>
+               : bp_decode_kernel<3, 3, 6, QEC_STOP_SYNDROME, ShiftsP7, ListTuneP7, 5>;
+}
 #elif defined(QEC_PHASE_TU)
 // The instrumented kernels of the shipped codes (QEC_OPT_PHASE_STATS, one wave per syndrome):
 // iters[] reports per sector soft | hard << 8 | agreed << 16 | jumped << 24 iterations.
@@ -1770,9 +1995,12 @@ struct Variant {
     KernelFn split[3];  // the same with one wave per sector (nullptr: not instantiated)
     KernelFn phase[3];  // QEC_OPT_PHASE_STATS: instrumented kernels (shipped codes only)
     int (*fill_tab0)(float pp, float* out);  // host iteration-0 tables (QEC_TABLE0_HOST)
+    uint32_t (*zero_out[2])(float pp, int N, int stop);  // per sector: zero-syndrome outcomes (zero_outcome)
     const char* name;
     KernelFn list = nullptr;  // syndrome stop, list mode (MODE 2: the sectors the triage passed on)
     int min_waves_syn = 1;    // its occupancy (waves per SIMD), for the list launch's grid
+    KernelFn list_sec[2] = {};        // the same per sector (MODE 5 / 6; QEC_LIST_SECTORS)
+    int list_waves[2] = {1, 1};       // their occupancies
     KernelFn seq[3][2] = {};     // sector launches (MODE 3 / 4): [stop][sector]
     long long seq_min_batch = 0;  // QEC_OPT_SECTOR_SPLIT = 1 takes the sector launches from this batch on (0: never)
 };
@@ -1800,6 +2028,7 @@ static Variant make_variant(int P, int S, int T, const char* name)
               {nullptr, nullptr, nullptr},
               {nullptr, nullptr, nullptr},
               fill_tab0<J, K, L>,
+              {zero_outcome<J, L>, zero_outcome<K, L>},
               name};
     if constexpr (WITH_SPLIT) {
         v.split[QEC_STOP_REF] = bp_decode_kernel<J, K, L, QEC_STOP_REF, SH, TU, 1>;
@@ -1810,10 +2039,16 @@ static Variant make_variant(int P, int S, int T, const char* name)
         v.seq[QEC_STOP_REF][1] = bp_decode_kernel<J, K, L, QEC_STOP_REF, SH, TU, 4>;
         v.seq[QEC_STOP_FIXED][0] = bp_decode_kernel<J, K, L, QEC_STOP_FIXED, SH, TU, 3>;
         v.seq[QEC_STOP_FIXED][1] = bp_decode_kernel<J, K, L, QEC_STOP_FIXED, SH, TU, 4>;
-        v.seq[QEC_STOP_SYNDROME][0] = bp_decode_kernel<J, K, L, QEC_STOP_SYNDROME, SH, TU, 3>;
-        v.seq[QEC_STOP_SYNDROME][1] = bp_decode_kernel<J, K, L, QEC_STOP_SYNDROME, SH, TU, 4>;
+        v.seq[QEC_STOP_SYNDROME][0] = bp_decode_kernel<J, K, L, QEC_STOP_SYNDROME, SH, SeqSynTune<TU>, 3>;
+        v.seq[QEC_STOP_SYNDROME][1] = bp_decode_kernel<J, K, L, QEC_STOP_SYNDROME, SH, SeqSynTune<TU>, 4>;
     }
     v.min_waves_syn = TUL::kMinWavesSyn;  // the list launch's grid (launch_decode_list)
+    if constexpr (WITH_SPLIT) {
+        v.list_sec[0] = bp_decode_kernel<J, K, L, QEC_STOP_SYNDROME, SH, TUL, 5>;
+        v.list_sec[1] = bp_decode_kernel<J, K, L, QEC_STOP_SYNDROME, SH, TUL, 6>;
+        v.list_waves[0] = TUL::kListMinWavesX;
+        v.list_waves[1] = TUL::kListMinWavesZ;
+    }
     return v;
 }
 // Tune<min waves per SIMD, relabel, zero-skip, short division, hard-message paths, sector split,
@@ -1857,7 +2092,7 @@ static Variant gen_p61()
             if (stop == QEC_STOP_SYNDROME && !QEC_P61_SYN_MINREG) continue;
             v.fn[stop] = p61_minreg_kernel(stop, false);
             v.split[stop] = p61_minreg_kernel(stop, true);
-            if (stop != QEC_STOP_SYNDROME)
+            if (stop != QEC_STOP_SYNDROME || QEC_SEQ_SYN_MINREG)
                 for (int sec = 0; sec < 2; ++sec) v.seq[stop][sec] = p61_minreg_seq_kernel(stop, sec);
         }
         // sector launches from 2^18 syndromes on: +1.3 % at 262 144, +0.3 % at 524 288, +1.9 % at 2^20,
@@ -1876,6 +2111,9 @@ static Variant gen_p7()
         v.split[QEC_STOP_SYNDROME] = p7_minreg_kernel(QEC_STOP_SYNDROME, true);
         v.list = p7_minreg_list_kernel();
         v.min_waves_syn = ListTuneP7::kMinWavesSyn;
+        for (int sec = 0; sec < 2; ++sec) v.list_sec[sec] = p7_minreg_list_sec_kernel(sec);
+        v.list_waves[0] = ListTuneP7::kListMinWavesX;
+        v.list_waves[1] = ListTuneP7::kListMinWavesZ;
     }
     return v;
 }
@@ -1997,6 +2235,8 @@ int launch_decode(const void* variant, const Code& c, const uint8_t* sX, const u
     a.hardPaths = hardPaths & (QEC_HP_FORMS | QEC_HP_CYCLE);
     a.scaled = scaled_ok(2.0f / 3.0f * errorProbability) ? 1 : 0;
     if (QEC_TABLE0_HOST) v->fill_tab0(2.0f / 3.0f * errorProbability, a.tab0);  // p' as the kernel forms it
+    if (QEC_ZERO_OUTCOME && !phase)
+        for (int sec = 0; sec < 2; ++sec) a.zs[sec] = v->zero_out[sec](2.0f / 3.0f * errorProbability, a.maxIter, stop);
     relabel(c.EX.data(), c.J, c.L, c.P, v->relabel, a.SX, a.DX, a.CX);
     relabel(c.EZ.data(), c.K, c.L, c.P, v->relabel, a.SZ, a.DZ, a.CZ);
     const int wavesPerBlock = v->waves_per_block;
@@ -2022,6 +2262,21 @@ int launch_decode(const void* variant, const Code& c, const uint8_t* sX, const u
 }
 
 bool decode_has_list(const void* variant) { return static_cast<const Variant*>(variant)->list != nullptr; }
+
+#if QEC_LIST_STAMPS
+}  // namespace qec
+// experiment builds: copies the 16 stamp words to out (host) and, with reset, zeroes them
+extern "C" int qec_debug_list_stamps(unsigned long long* out, int reset)
+{
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(qec::g_list_stamps), sizeof(unsigned long long) * 16) != hipSuccess) return 1;
+    if (reset) {
+        static const unsigned long long zero[16] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(qec::g_list_stamps), zero, sizeof zero) != hipSuccess) return 1;
+    }
+    return 0;
+}
+namespace qec {
+#endif
 
 // Compute units of the current device (4 SIMDs each), cached per device (the list-mode grid).
 static int device_cus()
@@ -2096,20 +2351,29 @@ int launch_decode_list(const void* variant, const Code& c, const uint8_t* sX, co
     if (QEC_TABLE0_HOST) v->fill_tab0(2.0f / 3.0f * errorProbability, a.tab0);
     relabel(c.EX.data(), c.J, c.L, c.P, v->relabel, a.SX, a.DX, a.CX);
     relabel(c.EZ.data(), c.K, c.L, c.P, v->relabel, a.SZ, a.DZ, a.CZ);
-    const long long need = (2 * B + a.G - 1) / a.G;  // waves for every sector
     static const long long rounds = [] {  // QEC_LIST_ROUNDS: grid in resident-slot rounds (experiments)
         const char* e = std::getenv("QEC_LIST_ROUNDS");
         const int v = e ? std::atoi(e) : 0;
         return (long long)(v >= 1 && v <= 64 ? v : 1);
     }();
-    const long long cap = 4LL * device_cus() * v->min_waves_syn * rounds;  // one per resident slot of the chip
-    const long long waves = need < cap ? need : cap;
     const int wpb = v->waves_per_block;
-    const long long blocks = (waves + wpb - 1) / wpb;
-    hipLaunchKernelGGL(v->list, dim3((unsigned)blocks), dim3(64 * wpb), 0, stream, a);
-    hipError_t err = hipGetLastError();
-    if (err != hipSuccess) return fail(QEC_ERR_HIP, std::string("bp_decode list launch: ") + hipGetErrorString(err));
-    return QEC_OK;
+    auto launch = [&](KernelFn fn, long long need, int waves_per_simd) -> int {
+        const long long cap = 4LL * device_cus() * waves_per_simd * rounds;  // one per resident slot of the chip
+        const long long waves = need < cap ? need : cap;
+        const long long blocks = (waves + wpb - 1) / wpb;
+        hipLaunchKernelGGL(fn, dim3((unsigned)blocks), dim3(64 * wpb), 0, stream, a);
+        const hipError_t err = hipGetLastError();
+        if (err != hipSuccess) return fail(QEC_ERR_HIP, std::string("bp_decode list launch: ") + hipGetErrorString(err));
+        return QEC_OK;
+    };
+    if (QEC_LIST_SECTORS && v->list_sec[0] && v->list_sec[1]) {
+        // listX in a kernel compiled for sector X alone, then listZ (the two merge their flags in the
+        // merge words, in either order)
+        const long long need = (B + a.G - 1) / a.G;  // waves for every sector of one list
+        const int rc = launch(v->list_sec[0], need, v->list_waves[0]);
+        return rc ? rc : launch(v->list_sec[1], need, v->list_waves[1]);
+    }
+    return launch(v->list, (2 * B + a.G - 1) / a.G, v->min_waves_syn);
 }
 
 #endif  // QEC_P61_MINREG_TU / QEC_PHASE_TU

@@ -53,14 +53,17 @@ def test_load_pmc_checks_workload_batch_and_build(tmp_path, monkeypatch):
     assert pm is not None and path.endswith("pmc_p61_4096_hp0.json")
 
 
-def test_valu_roofline_weighted_and_null():
+def test_valu_roofline_counter_exact_and_weighted():
+    """frac is the counter-exact SQ_INSTS_VALU issue; the cost-weighted figures (each transcendental at 4
+    and at 2 issue slots) sit beside it."""
     pm = {"valu_insts_per_syndrome": 1000.0, "valu_weighted_slots_per_syndrome": 1300.0, "batch": 1000,
-          "valu_trans_per_launch": 100000, "hbm_bytes_per_syndrome": 500.0}
+          "valu_trans_per_launch": 100000, "hbm_bytes_per_syndrome": 500.0, "lds_bank_conflict_share": 0.23}
     r = bench.valu_roofline(pm, os.path.join(ROOT, "profiles", "x.json"), 1000, 1.0)
     peak = 1024 * 2.4e9 / 2 / 1e12
-    assert abs(r["frac"] - 1300.0 * 1000 / 1e-3 / 1e12 / peak) < 1e-3
-    assert abs(r["frac_unweighted"] - 1000.0 * 1000 / 1e-3 / 1e12 / peak) < 1e-3
-    assert r["traffic"] == 500000
+    assert abs(r["frac"] - 1000.0 * 1000 / 1e-3 / 1e12 / peak) < 1e-3
+    assert abs(r["frac_weighted_probe4x"] - 1300.0 * 1000 / 1e-3 / 1e12 / peak) < 1e-3
+    assert abs(r["frac_weighted_guide2x"] - 1100.0 * 1000 / 1e-3 / 1e12 / peak) < 1e-3
+    assert r["traffic"] == 500000 and r["lds_bank_conflict_share"] == 0.23
     r = bench.valu_roofline(None, "no profile", 1000, 1.0)
     assert r["frac"] is None and "no PMC profile" in r["note"]
 

@@ -471,3 +471,26 @@ def test_one_launch_order_repeated(env, key, B):
         dec.set_option("schedule", 1)
     for r, it in outs[1:]:
         assert np.array_equal(r, outs[0][0]) and np.array_equal(it, outs[0][1])
+
+
+@pytest.mark.parametrize("key", ["P7", "P61"])
+@pytest.mark.parametrize("stop", ["fixed", "ref"])
+@pytest.mark.parametrize("N", [2, 3, 10, 11, 20, 21, 50])
+def test_zero_syndrome_outcome(env, key, stop, N):
+    """Zero-syndrome sectors under the fixed and reference stops take the launch's precomputed outcome
+    (bp_decode.hip, zero_outcome) when no final messages are requested: whole waves of zero syndromes,
+    zero X with nonzero Z and the reverse, mixed into nonzero rows, at p from 1e-4 to 1.4 (decisions,
+    convergence and syndrome flags of either value) -- against the oracle."""
+    code = env[key][0]
+    rng = np.random.default_rng(N)
+    for p in (1e-4, 0.01, 0.2, 0.74, 0.76, 1.4):
+        B = 200
+        x, z = depolarizing_errors(code.n, 7 * N, B, min(p, 0.3))
+        sX, sZ = code.syndrome(0, x), code.syndrome(1, z)
+        sX[:64] = 0
+        sZ[:64] = 0           # whole waves (P7: 9 per wave) of zero pairs
+        sX[64:100] = 0        # zero X, nonzero Z
+        sZ[100:130] = 0       # zero Z, nonzero X
+        pick = rng.random(B) < 0.3
+        sX[pick & (np.arange(B) >= 130)] = 0
+        check(env, key, sX, sZ, p, N, stop, want_q=False)

@@ -143,6 +143,9 @@ def main():
     if dur_ns and "SQ_INSTS_LDS" in avg:
         out["lds_issue_frac"] = round(avg["SQ_INSTS_LDS"] * 6 / (256 * 2.4e9) / (dur_ns * 1e-9), 4)
         out["lds_issue_basis"] = "SQ_INSTS_LDS x 6 CU-cycles (ds_bpermute_b32 price) / (256 CUs x 2.4 GHz x duration)"
+    if avg.get("SQ_ACTIVE_INST_LDS") and "SQ_LDS_BANK_CONFLICT" in avg:
+        # extra LDS cycles from bank conflicts over the cycles with an LDS instruction active
+        out["lds_bank_conflict_share"] = round(avg["SQ_LDS_BANK_CONFLICT"] / avg["SQ_ACTIVE_INST_LDS"], 4)
     if "SQ_WAIT_ANY" in avg and "SQ_ACTIVE_INST_ANY" in avg:
         out["wait_over_issue"] = round(avg["SQ_WAIT_ANY"] / max(avg["SQ_ACTIVE_INST_ANY"], 1), 4)
     with open(a.out, "w") as fh:

@@ -228,6 +228,10 @@ def main():
             dec.decode_bits_packed_dev(sXb, sZb, p, iters, args.stop, rec, its, stream=S["stream"])
 
         step = step_bits if bits else step_bytes
+        # the timed step: the same call with its tensors validated once (DecoderGPU.bind), so the host
+        # side of a step is the C ABI call alone
+        bound = (dec.bind(dec.decode_bits_packed_dev, sXb, sZb, p, iters, args.stop, rec, its, stream=stream) if bits
+                 else dec.bind(dec.decode_batch_packed_dev, sX, sZ, p, iters, args.stop, rec, its, stream=stream))
     else:
         eX = torch.empty((B, code.n), dtype=torch.uint8, device=dev)
         eZ = torch.empty((B, code.n), dtype=torch.uint8, device=dev)
@@ -237,9 +241,10 @@ def main():
         def step():
             dec.decode_batch_dev(sX, sZ, p, iters, args.stop, eX, eZ, fl, its, stream=S["stream"])
 
+        bound = dec.bind(dec.decode_batch_dev, sX, sZ, p, iters, args.stop, eX, eZ, fl, its, stream=stream)
+
     eager_step = step
-    if args.graph:
-        step = capture_graph(step, S, dev)
+    step = capture_graph(eager_step, S, dev) if args.graph else bound
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
@@ -296,6 +301,8 @@ def main():
         "p": p,
         "mean_iterations": {"X": round(it_mean[0], 4), "Z": round(it_mean[1], 4)},
         "decode_ms": round(kernel_ms, 4),
+        "decode_ms_basis": "GPU time of a step (dispatch order + decode launches): one HIP event pair on the launch "
+                           "stream around the timed steps, / steps",
     }
     pm, pm_path = load_pmc(args.code, iters, args.stop, p, B, args.hard_paths, args.input)
     out["roofline"] = valu_roofline(pm, pm_path, B, kernel_ms)
@@ -421,26 +428,27 @@ def relaunch(nproc):
 
 
 def timed_steps(step, steps, stream, dev, world):
-    """K steps between barrier + synchronize on both sides; wall time max over ranks, and the
-    mean decode-launch time from HIP events on the launch stream."""
+    """K steps between barrier + synchronize on both sides; wall time max over ranks, and the GPU time
+    of a step from one HIP event pair on the launch stream around the K steps (an event pair around
+    every step costs a P7 configs[1] step ~10 us of GPU time: tools/kbench/host_overhead.py)."""
     import torch
     import torch.distributed as dist
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
-    for k in range(steps):
-        ev[k][0].record(stream)
+    e0.record(stream)
+    for _ in range(steps):
         step()
-        ev[k][1].record(stream)
+    e1.record(stream)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
-    kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    kernel_ms = e0.elapsed_time(e1) / steps
     if world > 1:
         t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -483,22 +491,36 @@ def valu_roofline(pm, path, B, kernel_ms):
     return base
 
 
+def gpu_ms_per_step(step, stream, reps=3, window_ms=20.0):
+    """GPU time of one step: the median over reps of one HIP event pair around n back-to-back steps,
+    n enough for a ~window_ms window (a pair around each single step would add its own cost)."""
+    import torch
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record(stream)
+    step()
+    b.record(stream)
+    torch.cuda.synchronize()
+    n = max(1, int(math.ceil(window_ms / max(a.elapsed_time(b), 1e-3))))
+    ms = []
+    for _ in range(reps):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        for _ in range(n):
+            step()
+        b.record(stream)
+        torch.cuda.synchronize()
+        ms.append(a.elapsed_time(b) / n)
+    return float(np.median(ms))
+
+
 def retime_step(step, stream, B, outs, reps=3, world=1):
     """Time another step function on the same batch; outputs checked against the timed step's."""
     import torch
     import torch.distributed as dist
     ref = [t.clone() for t in outs]
     step()
-    ms = []
-    for _ in range(reps):
-        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        a.record(stream)
-        step()
-        b.record(stream)
-        torch.cuda.synchronize()
-        ms.append(a.elapsed_time(b))
+    k = gpu_ms_per_step(step, stream, reps)
     same = all(torch.equal(r, t) for r, t in zip(ref, outs))
-    k = float(np.median(ms))
     if world > 1:
         t = torch.tensor([k, 0.0 if same else 1.0], dtype=torch.float64, device=outs[0].device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -518,19 +540,11 @@ def retime(dec, step, stream, B, outs, opts, reps=3, world=1):
         dec.set_option(k, v)
     try:
         step()
-        ms = []
-        for _ in range(reps):
-            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            a.record(stream)
-            step()
-            b.record(stream)
-            torch.cuda.synchronize()
-            ms.append(a.elapsed_time(b))
+        k = gpu_ms_per_step(step, stream, reps)
     finally:
-        for k, v in old.items():
-            dec.set_option(k, v)
+        for k_, v in old.items():
+            dec.set_option(k_, v)
     same = all(torch.equal(r, t) for r, t in zip(ref, outs))
-    k = float(np.median(ms))
     if world > 1:
         t = torch.tensor([k, 0.0 if same else 1.0], dtype=torch.float64, device=outs[0].device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -634,15 +648,7 @@ def ref_stop(dec, sX, sZ, p, iters, B, stream, world, fname, check):
 
     step()
     torch.cuda.synchronize()
-    ms = []
-    for _ in range(5):
-        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        a.record(stream)
-        step()
-        b.record(stream)
-        torch.cuda.synchronize()
-        ms.append(a.elapsed_time(b))
-    k = float(np.median(ms))
+    k = gpu_ms_per_step(step, stream, 5)
     it = its.cpu().numpy()
     if world > 1:
         t = torch.tensor([k], dtype=torch.float64, device=sX.device)

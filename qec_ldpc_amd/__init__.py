@@ -388,6 +388,32 @@ class DecoderGPU:
         return rec, iters
 
     # ---- device buffers (torch tensors on this decoder's GPU) ---------------------------
+    _binding = False
+
+    def _issue(self, name, args):
+        """Calls the C entry point, or (inside bind) returns it with its checked arguments."""
+        fn = getattr(lib(), name)
+        if self._binding:
+            return fn, args, name
+        _check(fn(*args), name)
+
+    def bind(self, method, *args, **kw):
+        """A zero-argument callable that re-issues one device-buffer decode call (decode_batch_dev,
+        decode_batch_packed_dev or decode_bits_packed_dev) with these arguments: the tensors are
+        validated and their pointers taken once, so each call is only the C ABI call (for launch-bound
+        loops over the same buffers; the tensors must stay alive and unmoved)."""
+        self._binding = True
+        try:
+            fn, cargs, name = method(*args, **kw)
+        finally:
+            self._binding = False
+
+        def call():
+            rc = fn(*cargs)
+            if rc != 0:
+                raise QecError("%s failed (%d): %s" % (name, rc, last_error()))
+        return call
+
     def _stream(self, stream):
         if stream is None:
             import torch
@@ -430,7 +456,7 @@ class DecoderGPU:
                 self._t(eX, "eX", u8, (B, c.n)), self._t(eZ, "eZ", u8, (B, c.n)), self._t(flags, "flags", u8, (B,)),
                 self._t(iters, "iters", torch.int32, (B, 2), True),
                 self._t(q, "q", torch.float32, (B, (c.numEqsX + c.numEqsZ) * c.L), True))
-        _check(lib().qec_decode_batch_dev(self._h, *args, ctypes.c_void_p(self._stream(stream))), "qec_decode_batch_dev")
+        return self._issue("qec_decode_batch_dev", (self._h, *args, ctypes.c_void_p(self._stream(stream))))
 
     def decode_batch_packed_dev(self, sX, sZ, p, max_iter, stop, records, iters=None, q=None, stream=None):
         """Device-buffer batch decode into packed decision records [B, record_bytes()] (uint8)."""
@@ -444,8 +470,7 @@ class DecoderGPU:
                 self._t(records, "records", u8, (B, self.record_bytes())),
                 self._t(iters, "iters", torch.int32, (B, 2), True),
                 self._t(q, "q", torch.float32, (B, (c.numEqsX + c.numEqsZ) * c.L), True))
-        _check(lib().qec_decode_batch_packed_dev(self._h, *args, ctypes.c_void_p(self._stream(stream))),
-               "qec_decode_batch_packed_dev")
+        return self._issue("qec_decode_batch_packed_dev", (self._h, *args, ctypes.c_void_p(self._stream(stream))))
 
     def decode_bits_packed_dev(self, sXbits, sZbits, p, max_iter, stop, records, iters=None, q=None, stream=None):
         """Device-buffer decode of bit-row syndromes (int32 [B, ceil(m/32)] words, bit c of a row =
@@ -460,8 +485,7 @@ class DecoderGPU:
                 self._t(records, "records", torch.uint8, (B, self.record_bytes())),
                 self._t(iters, "iters", torch.int32, (B, 2), True),
                 self._t(q, "q", torch.float32, (B, (c.numEqsX + c.numEqsZ) * c.L), True))
-        _check(lib().qec_decode_bits_packed_dev(self._h, *args, ctypes.c_void_p(self._stream(stream))),
-               "qec_decode_bits_packed_dev")
+        return self._issue("qec_decode_bits_packed_dev", (self._h, *args, ctypes.c_void_p(self._stream(stream))))
 
     def sample_depolarizing_dev(self, seed, start, p, x, z, stream=None):
         """Device depolarising errors (the gap walk over Philox4x32-10 words, include/qec_ldpc.h)

@@ -39,6 +39,35 @@ def summarize(p, c, seconds, world):
     }
 
 
+def mc_roofline(p, samples, stop, iters, batch, code_name):
+    """The roofline of a sweep point from its rocprofv3 profile (profiles/pmc_mc_p61_p<p>.json,
+    tools/gpu/run_mc_profile.sh): per kernel its dispatch time and VALU / LDS issue fractions, and the
+    dominant kernel's bound -- only from a profile of this workload (p, samples, batch, stop, cap) taken
+    on this very build of the library (else the reason)."""
+    import qec_ldpc_amd as q
+    path = os.path.join(ROOT, "profiles", "pmc_mc_p61_p%g.json" % p)
+    try:
+        with open(path) as f:
+            pm = json.load(f)
+    except (OSError, ValueError):
+        return {"frac": None, "note": "no %s" % os.path.relpath(path, ROOT)}
+    if "P_61" not in code_name or (pm.get("stop"), pm.get("iters"), pm.get("samples"), pm.get("batch")) != \
+            (stop, iters, samples, batch):
+        return {"frac": None, "note": "%s: other workload" % os.path.basename(path)}
+    if pm.get("build_id") != q.build_id():
+        return {"frac": None, "note": "%s: collected on another build of the library" % os.path.basename(path)}
+    dom = pm["dominant"]
+    k = pm["kernels"][dom]
+    lds = k.get("lds_issue_frac") or 0.0
+    return {"dominant_kernel": dom, "bound": "lds" if lds > k.get("valu_issue_frac", 0.0) else "valu",
+            "frac": k.get("valu_issue_frac"), "lds_issue_frac": k.get("lds_issue_frac"),
+            "wait_over_issue": k.get("wait_over_issue"),
+            "kernels_us": {n: round(v["avg_ns"] / 1e3, 1) for n, v in pm["kernels"].items()},
+            "basis": "profiled dispatch times: SQ_INSTS_VALU x 2 / (1024 SIMDs x 2.4 GHz x time); LDS: SQ_INSTS_LDS "
+                     "x 6 CU-cycles / (256 CUs x 2.4 GHz x time)",
+            "profile": os.path.relpath(path, ROOT)}
+
+
 def reduce_counters(r, times, backend, dev):
     """Sums the per-rank counters and takes the max of the per-rank times across ranks (one
     all-reduce each, on the device for RCCL, on the host for gloo); without an initialised
@@ -121,6 +150,7 @@ def main():
         if backend:
             line["backend"] = backend
         line.update({"code": code.describe(), "stop": args.stop, "max_iters": args.iters, "seed": args.seed})
+        line["roofline"] = mc_roofline(p, hi - lo, args.stop, args.iters, args.batch, args.code)
         lines.append(line)
         if rank == 0:
             print(json.dumps(line), flush=True)

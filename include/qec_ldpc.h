@@ -178,8 +178,10 @@ int qec_decoder_device(const qec_decoder* dec);         /* HIP device ordinal (o
  *   QEC_OPT_SECTOR_SPLIT (default 1): the X and Z sectors of a syndrome are decoded by two
  *     waves instead of one after the other (halves the longest wave).  The launch then zeroes
  *     flags[] first and each sector ORs in its bits.  Bit-identical either way.  0 = off,
- *     1 = the kernel variant's measured choice (P7: split waves up to 2^20 syndromes; P61: sector
- *     launches from 2^18 on), 2 = on where the variant has split kernels (the two shipped codes),
+ *     1 = the kernel variant's measured choice (P7: split waves up to 2^20 syndromes, above 2^19 only
+ *     with the per-sector dispatch order; P61: sector launches from 2^18 on under the fixed stop, at 2^20
+ *     under the reference stop, at 2^20 and p >= 0.03 under the syndrome stop), 2 = on where the variant
+ *     has split kernels (the two shipped codes),
  *     3 = sector launches: two launches on the caller's stream, sector X then
  *     sector Z, each kernel compiled (and its registers allocated) for its own sector only; the Z
  *     launch ORs its flags into the byte the X launch stored (shipped codes; elsewhere as 0).

@@ -154,6 +154,19 @@ namespace qec {
 #ifndef QEC_SYN_SKIP_SEEN
 #define QEC_SYN_SKIP_SEEN 1
 #endif
+//   QEC_SYN_BALLOT   compile-time shifts: syndrome tests from ballots and scalar rotations (group_syndrome_ok)
+#ifndef QEC_SYN_BALLOT
+#define QEC_SYN_BALLOT 0
+#endif
+//   QEC_SYN_ROW0_FIRST  syndrome stop: test row 0 (lane-local with the relabelled tables) before the others
+#ifndef QEC_SYN_ROW0_FIRST
+#define QEC_SYN_ROW0_FIRST 1
+#endif
+//   QEC_IDENT_AGREE  a hard var pass whose every column took the agreeing-inputs shortcut counts as the
+//                    agreement path (the cycle jump's entry) where var_pass_agree is not run
+#ifndef QEC_IDENT_AGREE
+#define QEC_IDENT_AGREE 0
+#endif
 //   QEC_SCALED_DIV   var passes with at most 4 factors per fold divide guard-free on 2^32-scaled folds
 #ifndef QEC_SCALED_DIV
 #define QEC_SCALED_DIV 1
@@ -776,10 +789,14 @@ __device__ __forceinline__ bool short_domain(const float (&msg)[R][L], float pp,
 template <int R, int L, int SEC, bool LAST, bool HD, class SH, class TU, int CG = 1, bool ALLFAST = false,
           bool SOFT_IN = false>
 __device__ __forceinline__ uint32_t var_pass(const BpArgs& a, float (&msg)[R][L], const Lane& ln, float pp,
-                                             float one_minus_pp, bool& hard, bool& vagree, bool track = true)
+                                             float one_minus_pp, bool& hard, bool& vagree, bool track = true,
+                                             bool* ident = nullptr)
 {
     static_assert(L % CG == 0, "column groups must tile the L columns");
     const bool hard_in = !SOFT_IN && CG == 1 && hard;  // SOFT_IN: the caller knows the inputs are soft
+    // ident (out, hard inputs): every column took the agreeing-inputs shortcut below, i.e. the pass was the
+    // identity on the check-view registers -- the agreement path, found without var_pass_agree's gathers
+    bool all_done = hard_in;
     bool vsame = true;  // this lane's variables: all R outputs equal (float compare: NaN is unequal)
     uint32_t soft_bits = 0;  // OR of bits(q - q*q) over the outputs: 0 iff all are 0 or 1
     // the short division's guard assumes every message is a probability in [0, 1], which
@@ -847,6 +864,7 @@ __device__ __forceinline__ uint32_t var_pass(const BpArgs& a, float (&msg)[R][L]
                 }
             }
         }
+        all_done = band(all_done, done);
         if (!done) {
             // numerators / denominators of the outgoing messages, left folds in ascending k
             float num[CG][ND], den[CG][ND];
@@ -1003,6 +1021,7 @@ __device__ __forceinline__ uint32_t var_pass(const BpArgs& a, float (&msg)[R][L]
         hard = forms && all_live_sh<SH>(soft_bits == 0u, ln.live);
         vagree = hard && all_live_sh<SH>(vsame, ln.live);
     }
+    if (ident != nullptr) *ident = all_done;
     return hdmask;
 }
 
@@ -1069,6 +1088,55 @@ __device__ __forceinline__ bool lane_syndrome_ok(const BpArgs& a, uint32_t hdmas
     return match && !(sbits & kNonBinary);
 }
 
+// The same test for a whole group, from ballots instead of rotations (compile-time shifts): bit mu of
+// H_l = ballot(hard decision of column l) is variable (l, (mu + C[l]) mod P) of its group, so the
+// decision's syndrome on check-view lane lambda of row r is XOR_l H_l[(lambda + S[r][l]) mod P] -- a
+// cyclic rotation of each group's P bits of H_l by S[r][l], done in scalar registers.  The wave's
+// mismatches (input syndrome ballot XOR that, or a non-binary entry) then decide each group at once: no
+// ds_bpermute (R L of them in lane_syndrome_ok) and no VGPR temporaries.  Ballots see the lanes running
+// the call, i.e. the active groups; rotations stay inside a group, so other groups' bits never mix in.
+template <int P>
+__host__ __device__ constexpr unsigned long long group_bits_below(int s)  // bit g P + i for i < s, every group
+{
+    unsigned long long m = 0;
+    for (int g = 0; g < 64 / P; ++g)
+        for (int i = 0; i < s; ++i) m |= 1ull << (g * P + i);
+    return m;
+}
+template <int P>
+__device__ __forceinline__ unsigned long long rotr_groups(unsigned long long x, int s)  // bit gP+i <- bit gP+(i+s)%P
+{
+    if (s == 0) return x;
+    if constexpr (2 * P > 64) return (x >> s) | (x << (P - s));  // one group: bits >= P are cleared by the caller
+    else return ((x >> s) & group_bits_below<P>(P - s)) | ((x << (P - s)) & ~group_bits_below<P>(P - s));
+}
+template <int R, int L, int SEC, class SH>
+__device__ __forceinline__ bool group_syndrome_ok(const BpArgs& a, uint32_t hdmask, uint32_t sbits, const Lane& ln)
+{
+    if constexpr (SH::kStatic && QEC_SYN_BALLOT) {
+        constexpr int P = SH::kP;
+        unsigned long long H[L];
+#pragma unroll
+        for (int l = 0; l < L; ++l) H[l] = __ballot((hdmask >> l) & 1u);
+        unsigned long long bad = __ballot((sbits & kNonBinary) != 0u);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            unsigned long long syn = __ballot((sbits >> r) & 1u);
+#pragma unroll
+            for (int l = 0; l < L; ++l) syn ^= rotr_groups<P>(H[l], SH::template shift<SEC, L>(nullptr, r, l));
+            bad |= syn;
+        }
+        bad &= group_bits_below<P>(P);
+        if constexpr (2 * P > 64) {
+            return bad == 0ull;
+        } else {
+            return ((bad >> ln.gb) & ((1ull << P) - 1ull)) == 0ull;
+        }
+    } else {
+        return group_all_sh<SH>(lane_syndrome_ok<R, L, SEC, SH>(a, hdmask, sbits, ln), ln, SH::P(a));
+    }
+}
+
 // Whether a hard sector first tries the whole-sector agreement test (var_pass_agree, the entry to
 // the cycle jump).  Not for the syndrome stop rule: there it costs more than it saves -- with it the
 // P61 kernel spills at 128 VGPRs, without it P61 decodes 4-15 % faster at p = 0.1 .. 0.002 and P7
@@ -1081,6 +1149,20 @@ template <int STOP, class TU>
 constexpr bool kAgree()
 {
     return QEC_AGREE && (STOP != QEC_STOP_SYNDROME || QEC_AGREE_SYN || TU::kAgreeSyn);
+}
+
+// Row 0 of the syndrome test is lane-local when every block of row 0 has rotation 0 (the relabelled
+// compile-time tables: lane i of the variable view holds exactly the L variables of check (0, i)).
+template <int SEC, int L, class SH>
+constexpr bool kRow0Local()
+{
+    if constexpr (!SH::kStatic || !QEC_SYN_ROW0_FIRST) {
+        return false;
+    } else {
+        for (int l = 0; l < L; ++l)
+            if (SH::template shift<SEC, L>(nullptr, 0, l) != 0) return false;
+        return true;
+    }
 }
 
 // QEC_SYN_SKIP_SEEN for L columns (the never-seen marker ~0u is no decision mask when L < 32)
@@ -1109,10 +1191,16 @@ __device__ __forceinline__ bool iteration(const BpArgs& a, float (&msg)[R][L], u
     if (TU::kSaturate && hard) {
         check_pass_hard<R, L>(msg, sbits);  // outputs are hard too: hard stays set for the var pass
         agreed = kAgree<STOP, TU>() && (LAST || R >= 2) && var_pass_agree<R, L, SEC, HD, SH>(a, msg, ln, hdmask);
-        if (agreed)
+        if (agreed) {
             vagree = true;
-        else
-            hdmask = var_pass<R, L, SEC, LAST, HD, SH, TU>(a, msg, ln, pp, one_minus_pp, hard, vagree);
+        } else {
+            // without the agreement test (syndrome stop): a pass whose every column took the agreeing-inputs
+            // shortcut was the agreement path all the same (var_pass's ident), which the cycle jump needs
+            bool ident = false;
+            hdmask = var_pass<R, L, SEC, LAST, HD, SH, TU>(a, msg, ln, pp, one_minus_pp, hard, vagree, true,
+                                                           QEC_IDENT_AGREE ? &ident : nullptr);
+            agreed = ident;
+        }
     } else {
         check_pass<R, L, TU::kRowBarrier>(msg, sbits);
         // the hard-state test is skipped in the first QEC_TRACK_FROM iterations (they essentially
@@ -1153,10 +1241,20 @@ __device__ __forceinline__ bool iteration(const BpArgs& a, float (&msg)[R][L], u
                 return false;
             }
         }
-        // launder the bases again: the test's rotations are var_pass's return rotations, whose
-        // addresses would otherwise be kept live across the whole var pass for reuse here
-        if constexpr (SH::kMaskSelect && QEC_SYN_RELAUNDER) asm volatile("" : "+v"(ln.b0), "+v"(ln.b1));
-        const bool stop = group_all_sh<SH>(lane_syndrome_ok<R, L, SEC, SH>(a, hdmask, sbits, ln), ln, P);
+        // Row 0 first where it is lane-local (kRow0Local): a group that fails there fails the test, so
+        // when every active group does, rows 1 .. R - 1 (their rotations) are not needed
+        bool stop = false;
+        bool row0_fails = false;
+        if constexpr (kRow0Local<SEC, L, SH>()) {
+            const bool ok0 = ((__popc(hdmask) ^ sbits) & 1u) == 0u && !(sbits & kNonBinary);
+            row0_fails = all_live_sh<SH>(!group_all_sh<SH>(ok0, ln, P), ln.live);
+        }
+        if (!row0_fails) {
+            // launder the bases again: the test's rotations are var_pass's return rotations, whose
+            // addresses would otherwise be kept live across the whole var pass for reuse here
+            if constexpr (SH::kMaskSelect && QEC_SYN_RELAUNDER) asm volatile("" : "+v"(ln.b0), "+v"(ln.b1));
+            stop = group_syndrome_ok<R, L, SEC, SH>(a, hdmask, sbits, ln);
+        }
         if (kSkipSeen<L>() && !same0) {
             seen[1] = seen[0];
             seen[0] = hdmask;
@@ -1251,7 +1349,7 @@ __device__ __forceinline__ bool iteration0(const BpArgs& a, float (&msg)[R][L], 
             hdmask |= (uint32_t)((hdpat >> idx) & 1ull) << l;
             cv &= ((cvpat >> idx) & 1ull) != 0ull;
         }
-        const bool stop = group_all_sh<SH>(lane_syndrome_ok<R, L, SEC, SH>(a, hdmask, sbits, ln), ln, P);
+        const bool stop = group_syndrome_ok<R, L, SEC, SH>(a, hdmask, sbits, ln);
         hd_out = hdmask;
         cv_out = cv;
         msg_out = a.q != nullptr || __any(ln.live && !stop);  // q_final reads the messages
@@ -1294,7 +1392,7 @@ __device__ __forceinline__ bool iteration0(const BpArgs& a, float (&msg)[R][L], 
         return group_all_sh<SH>(lane_converged<R, L>(msg), ln, P);  // n = 0: DecoderCPU.h:287-290
     } else if constexpr (STOP == QEC_STOP_SYNDROME && !GO) {
         hd_out = hdmask;
-        return group_all_sh<SH>(lane_syndrome_ok<R, L, SEC, SH>(a, hdmask, sbits, ln), ln, P);
+        return group_syndrome_ok<R, L, SEC, SH>(a, hdmask, sbits, ln);
     }
     return false;
 }
@@ -1631,7 +1729,7 @@ __device__ __forceinline__ void decode_sector(const BpArgs& a, Lane& ln, uint32_
             }
             hdmask |= (uint32_t)hd << l;
         }
-        syn_ok = group_all_sh<SH>(lane_syndrome_ok<R, L, SEC, SH>(a, hdmask, sbits, ln), ln, P);
+        syn_ok = group_syndrome_ok<R, L, SEC, SH>(a, hdmask, sbits, ln);
     }
 #if QEC_LIST_STAMPS
     const unsigned long long ts3 = stamp_now();
@@ -2002,7 +2100,10 @@ struct Variant {
     KernelFn list_sec[2] = {};        // the same per sector (MODE 5 / 6; QEC_LIST_SECTORS)
     int list_waves[2] = {1, 1};       // their occupancies
     KernelFn seq[3][2] = {};     // sector launches (MODE 3 / 4): [stop][sector]
-    long long seq_min_batch = 0;  // QEC_OPT_SECTOR_SPLIT = 1 takes the sector launches from this batch on (0: never)
+    // QEC_OPT_SECTOR_SPLIT = 1 takes the sector launches from this batch on, per stop rule (0: never), and
+    // under the syndrome stop only from seq_syn_min_p on
+    long long seq_min_batch[3] = {};
+    float seq_syn_min_p = 0.0f;
 };
 
 // Both sectors' iteration-0 tables on the host, entry for entry what the device's table0_entry
@@ -2095,9 +2196,15 @@ static Variant gen_p61()
             if (stop != QEC_STOP_SYNDROME || QEC_SEQ_SYN_MINREG)
                 for (int sec = 0; sec < 2; ++sec) v.seq[stop][sec] = p61_minreg_seq_kernel(stop, sec);
         }
-        // sector launches from 2^18 syndromes on: +1.3 % at 262 144, +0.3 % at 524 288, +1.9 % at 2^20,
-        // but -2.7 % at 131 072 and -10 % at 65 536 (a second launch tail; profiles/r04/cmp_sector_launch_*.txt)
-        v.seq_min_batch = 1LL << 18;
+        // sector launches, fixed stop from 2^18 syndromes on: +1.3 % at 262 144, +0.3 % at 524 288, +1.9 % at
+        // 2^20, but -2.7 % at 131 072 and -10 % at 65 536 (a second launch tail; profiles/r04/cmp_sector_launch_*.txt);
+        // reference stop only at 2^20 (-2.3 % at 2^18, -0.8 % at 2^19, +0.7 % at 2^20); syndrome stop at 2^20 and
+        // p >= 0.03 (Monte-Carlo bit rows at 2^20: +1.8 % at p = 0.1, +1 % at 0.05, 0 at 0.02; byte rows at p = 0.01:
+        // -6 % at 2^18 and 2^20; profiles/r05/cmp_seq_per_stop*.txt)
+        v.seq_min_batch[QEC_STOP_FIXED] = 1LL << 18;
+        v.seq_min_batch[QEC_STOP_REF] = 1LL << 20;
+        v.seq_min_batch[QEC_STOP_SYNDROME] = 1LL << 20;
+        v.seq_syn_min_p = 0.03f;
     }
     return v;
 }
@@ -2171,12 +2278,25 @@ const void* select_variant(const Code& c, std::string& name)
 constexpr long long kSplitAutoMaxBatch = (1LL << 20) + 1;
 
 bool decode_uses_split(const void* variant, int stop, int split, long long B);
-// Sector launches (QEC_OPT_SECTOR_SPLIT = 3, or 1 from the variant's seq_min_batch on):
+// Sector launches (QEC_OPT_SECTOR_SPLIT = 3, or 1 as resolved by decode_sector_mode):
 // two launches, sector X then sector Z, each kernel compiled for its own sector (no merge words).
 static bool decode_uses_seq(const Variant* v, int stop, int split, long long B)
 {
-    return (split == 3 || (split == 1 && v->seq_min_batch > 0 && B >= v->seq_min_batch)) && v->seq[stop][0] != nullptr &&
-           v->seq[stop][1] != nullptr;
+    (void)B;
+    return split == 3 && v->seq[stop][0] != nullptr && v->seq[stop][1] != nullptr;
+}
+
+// QEC_OPT_SECTOR_SPLIT = 1 (the variant's measured choice) resolved for one launch: 3 (sector launches), 2
+// (split waves) or 0; other values are returned as they are
+int decode_sector_mode(const void* variant, int stop, int split, long long B, float p)
+{
+    const Variant* v = static_cast<const Variant*>(variant);
+    if (split != 1) return split;
+    const long long mb = v->seq_min_batch[stop];
+    if (mb > 0 && B >= mb && (stop != QEC_STOP_SYNDROME || p >= v->seq_syn_min_p) && v->seq[stop][0] != nullptr &&
+        v->seq[stop][1] != nullptr)
+        return 3;
+    return v->split_auto && B < kSplitAutoMaxBatch && v->split[stop] != nullptr ? 2 : 0;
 }
 
 bool decode_needs_merge(const void* variant, int stop, int split, long long B)
@@ -2189,7 +2309,7 @@ bool decode_uses_split(const void* variant, int stop, int split, long long B)
 {
     const Variant* v = static_cast<const Variant*>(variant);
     if (decode_uses_seq(v, stop, split, B)) return false;
-    return (split == 2 || (split == 1 && v->split_auto && B < kSplitAutoMaxBatch)) && v->split[stop] != nullptr;
+    return split == 2 && v->split[stop] != nullptr;
 }
 
 bool decode_has_phase_stats(const void* variant, int stop)

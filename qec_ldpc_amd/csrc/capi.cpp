@@ -27,6 +27,7 @@ int launch_schedule(const uint8_t* sX, const uint8_t* sZ, bool sbits, long long 
                     uint32_t* zero_merge, bool want_sectors, int32_t** perm_out, bool* sectors_out, hipStream_t st, int method, uint32_t* bar);
 bool decode_uses_split(const void* variant, int stop, int split, long long B);
 bool decode_needs_merge(const void* variant, int stop, int split, long long B);
+int decode_sector_mode(const void* variant, int stop, int split, long long B, float p);
 bool decode_has_list(const void* variant);
 bool decode_pattern_masks(const void* variant, float errorProbability, uint32_t pats[4]);
 int launch_decode_list(const void* variant, const Code& c, const uint8_t* sX, const uint8_t* sZ, long long B,
@@ -615,7 +616,9 @@ int dispatch_decode(qec_decoder* d, const uint8_t* sX, const uint8_t* sZ, long l
         d->last_path |= QEC_PATH_TRIAGE;
         return ws_release(d, st);
     }
-    int split_opt = d->sector_split;
+    // QEC_OPT_SECTOR_SPLIT = 1 resolved per launch (the variant's measured choice for this stop, batch and p)
+    int split_opt = decode_sector_mode(d->variant, stop, d->sector_split, B, p);
+    const bool split_auto = d->sector_split == 1;
     bool split = !d->phase_stats && decode_uses_split(d->variant, stop, split_opt, B);
     bool need_merge = !d->phase_stats && decode_needs_merge(d->variant, stop, split_opt, B);
     const bool single = 2 * c.P > 64;  // one syndrome per wave
@@ -627,7 +630,7 @@ int dispatch_decode(qec_decoder* d, const uint8_t* sX, const uint8_t* sZ, long l
     const int method = d->schedule == 3 ? QEC_ORDER_LOCAL : d->schedule == 4 ? QEC_ORDER_ONE_LAUNCH : QEC_ORDER_GLOBAL;
     // The tuned split above kSplitOrderedMinBatch was measured only with the per-sector order (round 2:
     // in total-weight order one wave per group won from 2^19 on); without that order keep one wave per group
-    if (split && split_opt == 1 && B > kSplitOrderedMinBatch &&
+    if (split && split_auto && B > kSplitOrderedMinBatch &&
         !(ordered && method == QEC_ORDER_GLOBAL && schedule_sector_order(B, sbits, c.mX, c.mZ))) {
         split_opt = 0;
         split = false;

@@ -213,19 +213,21 @@ def test_hard_paths_bit_identical(env, key, p):
 
 @pytest.mark.parametrize("key", ["P7", "P61"])
 @pytest.mark.parametrize("N", [5, 7, 11, 12, 20, 21, 33])
-def test_cycle_jump_bit_identical(env, key, N):
+@pytest.mark.parametrize("p", [0.01, 0.07])
+def test_cycle_jump_bit_identical(env, key, N, p):
     """QEC_OPT_CYCLE_JUMP (a hard sector whose last two iterations agreed jumps to its last
     iteration, bp_decode.hip cycle_end) changes no output bit: even and odd remaining counts,
-    the reference rule's next multiple of 10 before and after N - 1, every stop rule.  The
-    jump on equals the jump off, and both equal the oracle (final messages included)."""
+    the reference rule's next multiple of 10 before and after N - 1, every stop rule (p = 0.07: many
+    syndrome-stop sectors cycle without satisfying their syndrome and jump through var_pass's identity
+    passes).  The jump on equals the jump off, and both equal the oracle (final messages included)."""
     code, dec, _ = env[key]
-    x, z = depolarizing_errors(code.n, 4242 + N, 256, 0.01)
+    x, z = depolarizing_errors(code.n, 4242 + N, 256, p)
     sX, sZ = code.syndrome(0, x), code.syndrome(1, z)
     for stop in ("fixed", "ref", "syndrome"):
-        on = check(env, key, sX, sZ, 0.01, N, stop)
+        on = check(env, key, sX, sZ, p, N, stop)
         dec.set_option("cycle_jump", 0)
         try:
-            off = dec.decode_batch(sX, sZ, 0.01, N, stop, want_iters=True, want_q=True)
+            off = dec.decode_batch(sX, sZ, p, N, stop, want_iters=True, want_q=True)
         finally:
             dec.set_option("cycle_jump", 1)
         for a, b in zip(on[:4], off[:4]):
@@ -494,3 +496,46 @@ def test_zero_syndrome_outcome(env, key, stop, N):
         pick = rng.random(B) < 0.3
         sX[pick & (np.arange(B) >= 130)] = 0
         check(env, key, sX, sZ, p, N, stop, want_q=False)
+
+
+@pytest.mark.parametrize("p", [0.03, 0.07, 0.1])
+def test_syndrome_stop_sector_launches(env, p):
+    """The syndrome stop on a batch that takes the sector launches (P61, 2^18 syndromes: ordered, an X
+    and a Z launch, row-0-first tests, repeated-decision skips, identity-pass cycle jumps): the whole batch
+    equals the one-wave-per-syndrome launch in batch order and the launch with the cycle jump off, and a
+    slice (the heaviest syndromes of each sector among it) equals the oracle."""
+    import torch
+    from qec_ldpc_amd.gather import pack_records
+    code, _, orc = env["P61"]
+    B = 1 << 18
+    dev = torch.device("cuda", 0)
+    dec = q.DecoderGPU(code, 0, max_batch=B)
+    sX = torch.empty((B, code.numEqsX), dtype=torch.uint8, device=dev)
+    sZ = torch.empty((B, code.numEqsZ), dtype=torch.uint8, device=dev)
+    dec.sample_syndrome_dev(0xC0DE, 0, p, sX, sZ)
+
+    def run(**opts):
+        for k, v in opts.items():
+            dec.set_option(k, v)
+        rec = torch.empty((B, dec.record_bytes()), dtype=torch.uint8, device=dev)
+        its = torch.empty((B, 2), dtype=torch.int32, device=dev)
+        try:
+            dec.decode_batch_packed_dev(sX, sZ, p, 50, "syndrome", rec, its)
+            torch.cuda.synchronize()
+            return rec, its, dec.last_path()
+        finally:
+            for k in opts:
+                dec.set_option(k, 1)
+
+    rec, its, path = run()
+    assert "sector_launches" in path, sorted(path)
+    for opts in ({"schedule": 0, "sector_split": 0}, {"cycle_jump": 0}):
+        r2, i2, _ = run(**opts)
+        assert torch.equal(rec, r2) and torch.equal(its, i2), opts
+    hX, hZ = sX.cpu().numpy(), sZ.cpu().numpy()
+    wX, wZ = hX.sum(1, dtype=np.int64), hZ.sum(1, dtype=np.int64)
+    idx = np.unique(np.concatenate([np.arange(512), np.argsort(-wX, kind="stable")[:128],
+                                    np.argsort(-wZ, kind="stable")[:128]]))
+    o = orc.decode_batch(hX[idx], hZ[idx], p, 50, "syndrome")
+    assert np.array_equal(rec.cpu().numpy()[idx], pack_records(o[0], o[1], o[2]))
+    assert np.array_equal(its.cpu().numpy()[idx], o[3])

@@ -431,7 +431,10 @@ static int one_launch_capacity()
                 hipSuccess ||
             hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
             per_cu = cus = 0;
-        cap = per_cu > 0 && cus > 0 ? per_cu * cus : -1;  // -1: unknown, never take the one-launch form
+        // at most one workgroup per CU is counted: the occupancy API can report one workgroup per CU more
+        // than fits at some SGPR counts (MI355X_MICROARCH.md, correctness boundaries), and kOneLaunchChunks
+        // is below the CU count of a whole MI355X anyway
+        cap = per_cu > 0 && cus > 0 ? std::min(per_cu, 1) * cus : -1;  // -1: unknown, never take the one-launch form
         cached[dev].store(cap, std::memory_order_relaxed);
     }
     return cap;

@@ -500,10 +500,10 @@ def test_zero_syndrome_outcome(env, key, stop, N):
 
 @pytest.mark.parametrize("p", [0.03, 0.07, 0.1])
 def test_syndrome_stop_sector_launches(env, p):
-    """The syndrome stop on a batch that takes the sector launches (P61, 2^18 syndromes: ordered, an X
-    and a Z launch, row-0-first tests, repeated-decision skips, identity-pass cycle jumps): the whole batch
-    equals the one-wave-per-syndrome launch in batch order and the launch with the cycle jump off, and a
-    slice (the heaviest syndromes of each sector among it) equals the oracle."""
+    """The syndrome stop through the sector launches (P61, 2^18 syndromes, QEC_OPT_SECTOR_SPLIT 3: ordered,
+    an X and a Z launch, row-0-first tests, repeated-decision skips): the whole batch equals the
+    one-wave-per-syndrome launch in batch order, the sector launches with the cycle jump off and the
+    default choice, and a slice (the heaviest syndromes of each sector among it) equals the oracle."""
     import torch
     from qec_ldpc_amd.gather import pack_records
     code, _, orc = env["P61"]
@@ -527,9 +527,9 @@ def test_syndrome_stop_sector_launches(env, p):
             for k in opts:
                 dec.set_option(k, 1)
 
-    rec, its, path = run()
+    rec, its, path = run(sector_split=3)  # the sector launches (auto: at 2^20 and p >= 0.03)
     assert "sector_launches" in path, sorted(path)
-    for opts in ({"schedule": 0, "sector_split": 0}, {"cycle_jump": 0}):
+    for opts in ({"schedule": 0, "sector_split": 0}, {"sector_split": 3, "cycle_jump": 0}, {}):
         r2, i2, _ = run(**opts)
         assert torch.equal(rec, r2) and torch.equal(its, i2), opts
     hX, hZ = sX.cpu().numpy(), sZ.cpu().numpy()

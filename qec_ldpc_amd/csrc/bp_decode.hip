@@ -262,8 +262,9 @@ struct Tune {
 template <class TU>
 struct SeqSynTune : TU {
     static constexpr bool kAgreeSyn = QEC_SEQ_AGREE_SYN != 0;
-    static constexpr int kSeqSynWavesX = QEC_SEQ_SYN_MINW_X > 0 ? QEC_SEQ_SYN_MINW_X : TU::kMinWavesSyn;
-    static constexpr int kSeqSynWavesZ = QEC_SEQ_SYN_MINW_Z > 0 ? QEC_SEQ_SYN_MINW_Z : TU::kMinWavesSyn;
+    // the overrides only raise a variant's occupancy (P61 X: 4 -> 5 waves; P7 keeps its 7)
+    static constexpr int kSeqSynWavesX = QEC_SEQ_SYN_MINW_X > TU::kMinWavesSyn ? QEC_SEQ_SYN_MINW_X : TU::kMinWavesSyn;
+    static constexpr int kSeqSynWavesZ = QEC_SEQ_SYN_MINW_Z > TU::kMinWavesSyn ? QEC_SEQ_SYN_MINW_Z : TU::kMinWavesSyn;
 };
 
 //   QEC_LIST_MINW_P61 / _P7   min waves per SIMD of the list-mode kernels (ListTune); QEC_LIST_AGREE 0: no

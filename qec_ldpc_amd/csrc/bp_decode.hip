@@ -551,11 +551,23 @@ __device__ __forceinline__ int lane_i(const Lane& ln)
         return ln.i;
 }
 
+//   QEC_MASK_REMAT   one-group waves (P > 32): each rotation's lane mask is made at its use, s_bfm_b64 of the
+//                    shift, instead of a constant the compiler hoists out of the loops (where ~60 of them,
+//                    two SGPRs each, spill into VGPR lanes and come back with v_readlane)
+#ifndef QEC_MASK_REMAT
+#define QEC_MASK_REMAT 0
+#endif
 template <class SH>
 __device__ __forceinline__ int rot_addr(const Lane& ln, int s)
 {
     int base;
-    if constexpr (SH::kStatic && SH::kMaskSelect)
+    if constexpr (SH::kStatic && SH::kMaskSelect && QEC_MASK_REMAT && 2 * SH::kP > 64) {
+        int sv = s;
+        asm volatile("" : "+s"(sv));  // the shift is re-materialised here, so the mask is made here too
+        unsigned long long m;
+        asm("s_bfm_b64 %0, %1, 0" : "=s"(m) : "s"(sv));  // lanes below s: the group is lanes [0, P)
+        base = select_lanes(ln.b0, ln.b1, m);
+    } else if constexpr (SH::kStatic && SH::kMaskSelect)
         base = select_lanes(ln.b0, ln.b1, lanes_below<SH::kP>(s));
     else
         base = (ln.i < s) ? ln.b1 : ln.b0;  // loop-invariant per s: hoisted by the compiler

@@ -118,3 +118,15 @@ def test_non_binary_syndrome_entries(env, key, stop):
     f, ex, ez = dec.Decode(sx, sZ[b].astype(np.int32), 0.02, 12)
     r = orc.decode_batch(sX[b:b + 1], sZ[b:b + 1], 0.02, 12, "ref")  # Decode is the reference stop rule
     assert f == r[2][0] and np.array_equal(ex, r[0][0]) and np.array_equal(ez, r[1][0])
+
+
+def test_last_path_option_is_read_only(env):
+    """QEC_OPT_LAST_PATH (include/qec_ldpc.h) reports the last decode call's launch sequence and
+    cannot be set; the CPU engine's host decodes record no GPU launch form."""
+    code, dec, _ = env["P7"]
+    with pytest.raises(q.QecError):
+        dec.set_option("last_path", 1)
+    assert dec.get_option("last_path") == 0 and dec.last_path() == set()
+    x, z = depolarizing_errors(code.n, 0, 4, 0.02)
+    dec.decode_batch(code.syndrome(0, x), code.syndrome(1, z), 0.02, 5, "fixed")
+    assert dec.last_path() == set()

@@ -2019,7 +2019,7 @@ using ShiftsP7 = GeneratedShifts<3, 3, 6, 7, 2, 3, TuneP7::kRelabel, TuneP7::kMa
 #define QEC_P61_SYN_MINREG 0  // the P61 syndrome-stop kernels from the minreg unit too
 #endif
 #ifndef QEC_LIST_MINW_P61
-#define QEC_LIST_MINW_P61 3
+#define QEC_LIST_MINW_P61 4
 #endif
 #ifndef QEC_LIST_MINW_P7
 #define QEC_LIST_MINW_P7 5

@@ -137,6 +137,7 @@ struct qec_decoder {
     DeviceArray<int32_t> mit, midx;
     DeviceArray<unsigned long long> mcount;
     DeviceArray<unsigned long long> mpart;  // fused Monte-Carlo kernel: per-workgroup counter sums
+    PinnedArray<unsigned long long> mhost;  // the counters' host copy (page-locked: an asynchronous copy)
     EventSet mc_ev;  // qec_monte_carlo's ring of decode-time event pairs
     // multi-device group (qec_decoder_create_multi): the parts do the work, this handle only routes
     std::vector<qec_decoder*> parts;
@@ -934,11 +935,26 @@ int mc_batch(qec_decoder* d, McArgsHost h, int src, float p, int maxIter, int st
                                     want_iters ? d->mit.data() : nullptr, h.B, d->mcount.data(), st, rstride);
 }
 
+// Enqueues the counters' copy into the handle's page-locked host buffer (mhost); valid after the
+// stream has been synchronised.
+int mc_enqueue_counters(qec_decoder* d)
+{
+    try {
+        d->mhost.reserve(QEC_MC_NCOUNTERS_ALL);
+    } catch (const std::exception& ex) {
+        return fail(QEC_ERR_HIP, std::string("counter staging allocation: ") + ex.what());
+    }
+    QEC_HIP_CHECK(hipMemcpyAsync(d->mhost.data(), d->mcount.data(), QEC_MC_NCOUNTERS_ALL * sizeof(unsigned long long),
+                                 hipMemcpyDeviceToHost, d->stream));
+    return QEC_OK;
+}
+
 int mc_fetch_counters(qec_decoder* d, unsigned long long* out)
 {
-    QEC_HIP_CHECK(hipMemcpyAsync(out, d->mcount.data(), QEC_MC_NCOUNTERS_ALL * sizeof(unsigned long long),
-                                 hipMemcpyDeviceToHost, d->stream));
+    int rc = mc_enqueue_counters(d);
+    if (rc) return rc;
     QEC_HIP_CHECK(hipStreamSynchronize(d->stream));
+    std::memcpy(out, d->mhost.data(), QEC_MC_NCOUNTERS_ALL * sizeof(unsigned long long));
     return QEC_OK;
 }
 
@@ -976,6 +992,10 @@ int monte_carlo_part(qec_decoder* d, uint64_t seed, uint64_t start, uint64_t cou
     }
     if (k == 0)  // no batch zeroed the counters
         QEC_HIP_CHECK(hipMemsetAsync(d->mcount.data(), 0, QEC_MC_NCOUNTERS_ALL * sizeof(unsigned long long), st));
+    // the counters' copy behind the last batch, one synchronisation for the whole run; the remaining
+    // event pairs are complete by then (qec_monte_carlo reads the counters from mhost)
+    if ((rc = mc_enqueue_counters(d))) return rc;
+    QEC_HIP_CHECK(hipStreamSynchronize(st));
     for (uint64_t j = k > kRing ? k - kRing : 0; j < k; ++j)
         if ((rc = harvest(j % kRing))) return rc;
     *decode_s = dec;
@@ -1188,11 +1208,8 @@ int qec_monte_carlo(qec_decoder* d, uint64_t seed, uint64_t start, uint64_t coun
     unsigned long long cn[QEC_MC_NCOUNTERS_ALL] = {};
     for (int j = 0; j < np; ++j) {
         if (rcs[j]) return fail(rcs[j], "part " + std::to_string(j) + ": " + errs[j]);
-        QEC_DEVICE_SCOPE(parts[j]->device);
-        unsigned long long part[QEC_MC_NCOUNTERS_ALL];
-        const int rc = mc_fetch_counters(parts[j], part);
-        if (rc) return rc;
-        for (int k = 0; k < QEC_MC_NCOUNTERS_ALL; ++k) cn[k] += part[k];
+        // monte_carlo_part left the part's counters in its page-locked copy, its stream synchronised
+        for (int k = 0; k < QEC_MC_NCOUNTERS_ALL; ++k) cn[k] += parts[j]->mhost[k];
     }
     const auto t1 = std::chrono::high_resolution_clock::now();
     out->tested = count;

@@ -22,7 +22,11 @@ def test_committed_profiles_are_well_formed():
         with open(os.path.join(ROOT, "profiles", name)) as f:
             pm = json.load(f)
         assert len(pm["build_id"]) == 16 and pm["batch"] > 0 and pm["stop"] in ("fixed", "ref", "syndrome"), name
-        assert pm["valu_insts_per_syndrome"] > 0 and pm["valu_weighted_slots_per_syndrome"] > 0, name
+        if name.startswith("pmc_mc_"):  # config-5 kernel profiles (tools/gpu/mc_pmc_summary.py)
+            assert pm["dominant"] in pm["kernels"] and pm["samples"] > 0, name
+            assert all(k["avg_ns"] > 0 and k.get("valu_issue_frac") is not None for k in pm["kernels"].values()), name
+        else:  # decode-launch profiles (tools/gpu/pmc_summary.py)
+            assert pm["valu_insts_per_syndrome"] > 0 and pm["valu_weighted_slots_per_syndrome"] > 0, name
 
 
 def test_load_pmc_checks_workload_batch_and_build(tmp_path, monkeypatch):

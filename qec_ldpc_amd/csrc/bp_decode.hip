@@ -167,6 +167,11 @@ namespace qec {
 #ifndef QEC_IDENT_AGREE
 #define QEC_IDENT_AGREE 0
 #endif
+//   QEC_SYN_DEFER_RETURN  syndrome stop, one group per wave: a var pass leaves its outputs in the variable view
+//                         and rotates them back to the check view only when the sector goes on (defer_return)
+#ifndef QEC_SYN_DEFER_RETURN
+#define QEC_SYN_DEFER_RETURN 1
+#endif
 //   QEC_SCALED_DIV   var passes with at most 4 factors per fold divide guard-free on 2^32-scaled folds
 #ifndef QEC_SCALED_DIV
 #define QEC_SCALED_DIV 1
@@ -784,6 +789,35 @@ __device__ __forceinline__ bool short_domain(const float (&msg)[R][L], float pp,
     return band(all_live_sh<SH>(__float_as_uint(b) >= __float_as_uint(0x1p-98f), live), zero_ok<R, LAST>(pp));
 }
 
+// Syndrome stop with one group per wave (compile-time P > 32): the var pass stores its outgoing messages
+// in the variable view (msg[r][l] = variable (l, .)'s message on edge r) instead of rotating each back to
+// its check at once.  The stop test needs only the decisions, and the post-processing of a stopped
+// sector only the decisions and "every message outside (0.01, 0.99)", which does not depend on the
+// layout; so the R L return rotations run (return_pass) only when the sector goes on (or its final
+// messages are requested).  At low p most listed sectors stop after one soft iteration.
+template <bool HD, class SH>
+constexpr bool defer_return()
+{
+    if constexpr (SH::kStatic) return HD && QEC_SYN_DEFER_RETURN && 2 * SH::kP > 64;
+    else return false;
+}
+
+// The check view of the messages a deferring var pass left in the variable view.
+template <int R, int L, int SEC, class SH>
+__device__ __forceinline__ void return_pass(const BpArgs& a, float (&msg)[R][L], Lane& ln)
+{
+    const int P = SH::P(a);
+    const int* et = SH::template table<SEC>(a);
+    if constexpr (SH::kMaskSelect) asm volatile("" : "+v"(ln.b0), "+v"(ln.b1));
+#pragma unroll
+    for (int l = 0; l < L; ++l)
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int sh = SH::template shift<SEC, L>(et, r, l);
+            msg[r][l] = rot<SH>(msg[r][l], ln, sh == 0 ? 0 : P - sh);
+        }
+}
+
 // VarNodeUpdate (DecoderCPU.h:188-229) for variables (l, i): gather the R incoming
 // check messages by forward rotation, update, scatter back by the inverse rotation.
 // LAST: the final iteration includes the self message (DecoderCPU.h:216).
@@ -1024,7 +1058,7 @@ __device__ __forceinline__ uint32_t var_pass(const BpArgs& a, float (&msg)[R][L]
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 const int sh = SH::template shift<SEC, L>(et, r, l);
-                msg[r][l] = rot<SH>(qv[c][r], ln, sh == 0 ? 0 : P - sh);
+                msg[r][l] = defer_return<HD, SH>() ? qv[c][r] : rot<SH>(qv[c][r], ln, sh == 0 ? 0 : P - sh);
             }
         }
         if constexpr (QEC_COL_BARRIER) __builtin_amdgcn_sched_barrier(0);  // see QEC_COL_BARRIER
@@ -1201,11 +1235,13 @@ __device__ __forceinline__ bool iteration(const BpArgs& a, float (&msg)[R][L], u
     uint32_t hdmask = 0;
     agreed = false;
     vagree = false;
+    bool var_layout = defer_return<HD, SH>();  // the messages are left in the variable view (defer_return)
     if (TU::kSaturate && hard) {
         check_pass_hard<R, L>(msg, sbits);  // outputs are hard too: hard stays set for the var pass
         agreed = kAgree<STOP, TU>() && (LAST || R >= 2) && var_pass_agree<R, L, SEC, HD, SH>(a, msg, ln, hdmask);
         if (agreed) {
             vagree = true;
+            var_layout = false;  // the agreement path leaves the check-view registers as they are
         } else {
             // without the agreement test (syndrome stop): a pass whose every column took the agreeing-inputs
             // shortcut was the agreement path all the same (var_pass's ident), which the cycle jump needs
@@ -1244,25 +1280,19 @@ __device__ __forceinline__ bool iteration(const BpArgs& a, float (&msg)[R][L], u
         // decision or alternate between two).  seen[] holds whole-group tested states: it is updated
         // group-uniformly (kept when the decision is seen[0], else pushed).
         const bool same0 = kSkipSeen<L>() && group_all_sh<SH>(hdmask == seen[0], ln, P);
-        if constexpr (kSkipSeen<L>()) {
-            const bool same1 = group_all_sh<SH>(hdmask == seen[1], ln, P);
-            if (all_live_sh<SH>(same0 || same1, ln.live)) {
-                if (!same0) {
-                    seen[1] = seen[0];
-                    seen[0] = hdmask;
-                }
-                return false;
-            }
-        }
+        bool skip = false;
+        if constexpr (kSkipSeen<L>()) skip = all_live_sh<SH>(same0 || group_all_sh<SH>(hdmask == seen[1], ln, P), ln.live);
         // Row 0 first where it is lane-local (kRow0Local): a group that fails there fails the test, so
         // when every active group does, rows 1 .. R - 1 (their rotations) are not needed
         bool stop = false;
         bool row0_fails = false;
         if constexpr (kRow0Local<SEC, L, SH>()) {
-            const bool ok0 = ((__popc(hdmask) ^ sbits) & 1u) == 0u && !(sbits & kNonBinary);
-            row0_fails = all_live_sh<SH>(!group_all_sh<SH>(ok0, ln, P), ln.live);
+            if (!skip) {
+                const bool ok0 = ((__popc(hdmask) ^ sbits) & 1u) == 0u && !(sbits & kNonBinary);
+                row0_fails = all_live_sh<SH>(!group_all_sh<SH>(ok0, ln, P), ln.live);
+            }
         }
-        if (!row0_fails) {
+        if (!skip && !row0_fails) {
             // launder the bases again: the test's rotations are var_pass's return rotations, whose
             // addresses would otherwise be kept live across the whole var pass for reuse here
             if constexpr (SH::kMaskSelect && QEC_SYN_RELAUNDER) asm volatile("" : "+v"(ln.b0), "+v"(ln.b1));
@@ -1272,6 +1302,9 @@ __device__ __forceinline__ bool iteration(const BpArgs& a, float (&msg)[R][L], u
             seen[1] = seen[0];
             seen[0] = hdmask;
         }
+        // a deferring pass: the check view is needed when the sector goes on to another iteration (one
+        // group per wave, so stop is wave-uniform) or its final messages are requested
+        if (var_layout && (a.q != nullptr || (!LAST && !stop))) return_pass<R, L, SEC, SH>(a, msg, ln);
         return stop;
     }
     return false;

@@ -110,14 +110,15 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # this rank's GPU first, so RCCL's communicator and the barriers run on it
+    local = local % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(local)
     backend = None
     if world > 1:
         # RCCL ("nccl") over xGMI; QEC_BENCH_BACKEND=gloo rehearses the multi-rank path with several
         # ranks sharing one GPU (RCCL needs one GPU per rank)
         backend = os.environ.get("QEC_BENCH_BACKEND") or "nccl"
         dist.init_process_group(backend)
-    local = local % max(1, torch.cuda.device_count())
-    torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     code = q.Quantum_LDPC_Code.createFromFile(code_path(args.code))
     dec = q.DecoderGPU(code, local)

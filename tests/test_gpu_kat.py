@@ -113,3 +113,26 @@ def test_cli_drop_in(tmp_path, code_paths, flags):
     assert int(fields["Errors Tested"]) == 2000 and int(fields["Error Weight"]) == 2
     assert "Run complete." in (tmp_path / "output_log.txt").read_text()
 
+
+
+@pytest.mark.parametrize("stop,flags", [("syndrome", []), ("ref", ["--devices", "0,0"]), ("fixed", ["--batch", "4096"])])
+def test_cli_philox_runs(tmp_path, code_paths, decoders, stop, flags):
+    """--rng philox: COUNT depolarising samples at p (qec_monte_carlo) -> one results block whose
+    counters equal the library's Monte-Carlo run on the same Philox stream, for every stop rule,
+    device list and batch size."""
+    (tmp_path / "results").mkdir()
+    (tmp_path / "init.txt").write_text("%s 1 1 20000 30 0.02\n" % code_paths["P7"])
+    r = subprocess.run([os.path.join(ROOT, "tools", "qec_ldpc"), "--rng", "philox", "--stop", stop,
+                        "--seed", "0x51EC0DE"] + flags + ["init.txt"],
+                       cwd=tmp_path, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    files = os.listdir(tmp_path / "results")
+    assert files == ["[J=3,K=3,L=6,P=7,s=2,t=3][[n=42,k=0]]_DEPOLARIZING_MAX_30_p_0.02_%s.txt" % stop]
+    fields = dict(re.findall(r"^([A-Za-z ()\-]+): (.*)$", (tmp_path / "results" / files[0]).read_text(), flags=re.M))
+    want = decoders["P7"].monte_carlo(0x51EC0DE, 0, 20000, 0.02, 30, stop)
+    names = {"tested": "Errors Tested", "withX": "Errors With X", "withZ": "Errors With Z",
+             "corrected": "Corrected", "synX": "Syndrome Errors X", "synZ": "Syndrome Errors Z",
+             "logical": "Logical Errors", "convX": "Convergence Fail X", "convZ": "Convergence Fail Z",
+             "iterationsX": "Iterations X", "iterationsZ": "Iterations Z"}
+    assert {k: int(fields[v]) for k, v in names.items()} == {k: want[k] for k in names}
+    assert want["tested"] == 20000 and fields["Stop Rule"] == stop

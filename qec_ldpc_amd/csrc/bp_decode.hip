@@ -321,17 +321,52 @@ constexpr int col_group()
     return g;
 }
 
+//   QEC_ROT_PUSH   one-group waves (32 < P < 64): a rotation whose pull wraps inside a 32-lane half
+//                  (source lane i - s + P for i < s, with s <= 31) is made as the same rotation pushed
+//                  instead (ds_permute_b32, lane i to lane i + s mod P).  A wrapping ds_bpermute puts two
+//                  sources of its first half on one LDS bank and costs 7.1 instead of 6.1 cycles; a push
+//                  of any shift costs 6.1 (tools/kbench/perm_probe.hip, profiles/r05/perm_probe.txt).  The
+//                  group then sits on the TOP P lanes of the wave, [64 - P, 64), and the 64 - P idle lanes
+//                  below it: when several lanes push to one lane the highest-numbered source wins (the ISA's
+//                  DS_PERMUTE_B32 rule; tools/kbench/permute_collide.hip checks it on the chip), so an idle
+//                  lane's push never overwrites a group lane's (the group's pushes are a bijection on it).
+#ifndef QEC_ROT_PUSH
+#define QEC_ROT_PUSH 1
+#endif
+
+// The group's first lane in a one-group wave (compile-time 32 < P < 64): 64 - P with pushed rotations
+// (QEC_ROT_PUSH), else 0.
+template <int P_>
+constexpr int one_group_base()
+{
+    return (QEC_ROT_PUSH && 2 * P_ > 64 && P_ < 64) ? 64 - P_ : 0;
+}
+
+// Rotations by push (QEC_ROT_PUSH) for one-group waves with lane-mask rotation bases
+template <class SH>
+constexpr bool kPushRot()
+{
+    return QEC_ROT_PUSH && SH::kStatic && SH::kMaskSelect && 2 * SH::kP > 64 && SH::kP < 64;
+}
+// where the one group starts (kPushRot: the top lanes)
+template <class SH>
+constexpr int kGroupBase()
+{
+    if constexpr (kPushRot<SH>()) return 64 - SH::kP;
+    return 0;
+}
+
 // true iff pred holds on every live lane of the wave (lanes outside the batch, or masked off
 // by a finished group, do not vote)
 __device__ __forceinline__ bool all_live(bool pred, bool live) { return __ballot(live && !pred) == 0ull; }
 // The same for a shift provider: with compile-time P > 32 a wave holds one syndrome group whose
-// lanes [0, P) are all live once the wave runs (a wave with no syndrome of the batch returns
+// lanes [kGroupBase, kGroupBase + P) are all live once the wave runs (a wave with no syndrome of the batch returns
 // at entry), so liveness is a constant lane mask instead of a per-lane predicate.
 template <class SH>
 __device__ __forceinline__ bool all_live_sh(bool pred, bool live)
 {
     if constexpr (SH::kStatic && 2 * SH::kP > 64) {
-        constexpr unsigned long long gm = SH::kP >= 64 ? ~0ull : ((1ull << SH::kP) - 1ull);
+        constexpr unsigned long long gm = (SH::kP >= 64 ? ~0ull : ((1ull << SH::kP) - 1ull)) << kGroupBase<SH>();
         return (__ballot(!pred) & gm) == 0ull;
     } else {
         return all_live(pred, live);
@@ -529,14 +564,16 @@ struct Lane {
     bool live;   // lane belongs to a syndrome of this batch
 };
 
+// lanes [g P, g P + s) of every group g (of the one group's [64 - P, 64 - P + s) at the top lanes)
 template <int P_>
 __device__ constexpr unsigned long long lanes_below(int s)
 {
     unsigned long long m = 0;
     for (int g = 0; g < 64 / P_; ++g)
         for (int k = 0; k < s; ++k) m |= 1ull << (g * P_ + k);
-    return m;
+    return m << one_group_base<P_>();
 }
+
 
 __device__ __forceinline__ int select_lanes(int a, int b, unsigned long long m)
 {
@@ -550,7 +587,10 @@ __device__ __forceinline__ int select_lanes(int a, int b, unsigned long long m)
 template <class SH>
 __device__ __forceinline__ int lane_i(const Lane& ln)
 {
-    if constexpr (SH::kStatic)
+    if constexpr (kPushRot<SH>()) {
+        const int lane = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+        return lane < kGroupBase<SH>() ? lane : lane - kGroupBase<SH>();  // the group on the top lanes
+    } else if constexpr (SH::kStatic)
         return (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)) % SH::kP;
     else
         return ln.i;
@@ -570,7 +610,7 @@ __device__ __forceinline__ int rot_addr(const Lane& ln, int s)
         int sv = s;
         asm volatile("" : "+s"(sv));  // the shift is re-materialised here, so the mask is made here too
         unsigned long long m;
-        asm("s_bfm_b64 %0, %1, 0" : "=s"(m) : "s"(sv));  // lanes below s: the group is lanes [0, P)
+        asm("s_bfm_b64 %0, %1, %2" : "=s"(m) : "s"(sv), "s"(kGroupBase<SH>()));  // the group's lanes below s
         base = select_lanes(ln.b0, ln.b1, m);
     } else if constexpr (SH::kStatic && SH::kMaskSelect)
         base = select_lanes(ln.b0, ln.b1, lanes_below<SH::kP>(s));
@@ -582,6 +622,14 @@ __device__ __forceinline__ int rot_addr(const Lane& ln, int s)
 template <class SH>
 __device__ __forceinline__ float rot(float v, const Lane& ln, int s)
 {
+    if constexpr (kPushRot<SH>()) {
+        if (s != 0 && s <= 31) {
+            // the same rotation as a push: lane i's value goes to lane (i + s) mod P.  The address is
+            // (i < P - s ? b1 : b0) + (256 + 4 s - 4 P): lane (i + s) or (i + s - P), mod 64
+            const int base = select_lanes(ln.b0, ln.b1, lanes_below<SH::kP>(SH::kP - s));
+            return __int_as_float(__builtin_amdgcn_ds_permute(base + (256 + 4 * s - 4 * SH::kP), __float_as_int(v)));
+        }
+    }
     return s == 0 ? v : bperm(rot_addr<SH>(ln, s), v);
 }
 template <class SH>
@@ -599,13 +647,13 @@ __device__ __forceinline__ bool group_all(bool pred, int gb, int P)
     return (bad & gm) == 0ull;
 }
 // The same for a shift provider: with compile-time P > 32 a wave holds one group (lanes
-// [0, P); the lanes above are never live), so the group mask is a constant rather than a
+// [kGroupBase, kGroupBase + P); the other lanes are never live), so the group mask is a constant rather than a
 // per-lane 64-bit value kept live across the whole kernel.
 template <class SH>
 __device__ __forceinline__ bool group_all_sh(bool pred, const Lane& ln, int P)
 {
     if constexpr (SH::kStatic && 2 * SH::kP > 64) {
-        constexpr unsigned long long gm = SH::kP >= 64 ? ~0ull : ((1ull << SH::kP) - 1ull);
+        constexpr unsigned long long gm = (SH::kP >= 64 ? ~0ull : ((1ull << SH::kP) - 1ull)) << kGroupBase<SH>();
         return (__ballot(!pred) & gm) == 0ull;
     } else {
         return group_all(pred, ln.gb, P);
@@ -1914,9 +1962,12 @@ void bp_decode_kernel(const BpArgs a)
     const long long wave = (long long)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     const int P = SH::P(a);
     const int G = SH::kStatic ? 64 / P : a.G;
-    const int g = lane / P;
-    const int i = lane - g * P;
-    const int gb = g * P;
+    // with pushed rotations the one group sits on lanes [64 - P, 64); the idle lanes below it take
+    // group index 1 (never in range) and in-group indices 0 .. 63 - P (in bounds, never stored)
+    constexpr int kGB = kGroupBase<SH>();
+    const int g = kGB ? (lane < kGB ? 1 : 0) : lane / P;
+    const int i = kGB ? (lane < kGB ? lane : lane - kGB) : lane - g * P;
+    const int gb = kGB ? kGB : g * P;
     // iteration-0 tables of both sectors (iteration0), built by the workgroup before any wave leaves
     constexpr int kTabX = (1 << RX) * RX, kTabZ = (1 << RZ) * RZ;
     __shared__ float tab0[QEC_TABLE0 ? kTabX + kTabZ : 1];

@@ -334,25 +334,26 @@ constexpr int col_group()
 #define QEC_ROT_PUSH 1
 #endif
 
-// The group's first lane in a one-group wave (compile-time 32 < P < 64): 64 - P with pushed rotations
-// (QEC_ROT_PUSH), else 0.
+// The first lane of group 0 for compile-time P: with pushed rotations (QEC_ROT_PUSH) the G = 64 / P
+// groups take the top G P lanes and the 64 - G P idle lanes sit below them, else the groups start at lane 0.
 template <int P_>
-constexpr int one_group_base()
+constexpr int group_base()
 {
-    return (QEC_ROT_PUSH && 2 * P_ > 64 && P_ < 64) ? 64 - P_ : 0;
+    return (QEC_ROT_PUSH && 2 * P_ > 64 && P_ < 64) ? 64 - (64 / P_) * P_ : 0;
 }
 
-// Rotations by push (QEC_ROT_PUSH) for one-group waves with lane-mask rotation bases
+// Rotations by push (QEC_ROT_PUSH) for compile-time one-group waves.  The code also handles several
+// groups per wave (every shift pushed, groups on the top lanes), but for P7 it measured -1.8 .. +0.5 %
+// (profiles/r05/cmp_rot_push.txt), so multi-group waves keep their pulls.
 template <class SH>
 constexpr bool kPushRot()
 {
-    return QEC_ROT_PUSH && SH::kStatic && SH::kMaskSelect && 2 * SH::kP > 64 && SH::kP < 64;
+    return QEC_ROT_PUSH && SH::kStatic && 2 * SH::kP > 64 && SH::kP < 64;
 }
-// where the one group starts (kPushRot: the top lanes)
 template <class SH>
 constexpr int kGroupBase()
 {
-    if constexpr (kPushRot<SH>()) return 64 - SH::kP;
+    if constexpr (kPushRot<SH>()) return group_base<SH::kP>();
     return 0;
 }
 
@@ -564,14 +565,14 @@ struct Lane {
     bool live;   // lane belongs to a syndrome of this batch
 };
 
-// lanes [g P, g P + s) of every group g (of the one group's [64 - P, 64 - P + s) at the top lanes)
+// lanes [g P, g P + s) of every group g, from group_base (the top lanes with pushed rotations)
 template <int P_>
 __device__ constexpr unsigned long long lanes_below(int s)
 {
     unsigned long long m = 0;
     for (int g = 0; g < 64 / P_; ++g)
         for (int k = 0; k < s; ++k) m |= 1ull << (g * P_ + k);
-    return m << one_group_base<P_>();
+    return m << group_base<P_>();
 }
 
 
@@ -587,9 +588,12 @@ __device__ __forceinline__ int select_lanes(int a, int b, unsigned long long m)
 template <class SH>
 __device__ __forceinline__ int lane_i(const Lane& ln)
 {
-    if constexpr (kPushRot<SH>()) {
+    if constexpr (kPushRot<SH>() && kGroupBase<SH>() > 0) {
         const int lane = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
-        return lane < kGroupBase<SH>() ? lane : lane - kGroupBase<SH>();  // the group on the top lanes
+        if constexpr (2 * SH::kP > 64)
+            return lane < kGroupBase<SH>() ? lane : lane - kGroupBase<SH>();  // the group on the top lanes
+        else
+            return lane < kGroupBase<SH>() ? lane : (lane - kGroupBase<SH>()) % SH::kP;
     } else if constexpr (SH::kStatic)
         return (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)) % SH::kP;
     else
@@ -620,22 +624,26 @@ __device__ __forceinline__ int rot_addr(const Lane& ln, int s)
 }
 
 template <class SH>
-__device__ __forceinline__ float rot(float v, const Lane& ln, int s)
-{
-    if constexpr (kPushRot<SH>()) {
-        if (s != 0 && s <= 31) {
-            // the same rotation as a push: lane i's value goes to lane (i + s) mod P.  The address is
-            // (i < P - s ? b1 : b0) + (256 + 4 s - 4 P): lane (i + s) or (i + s - P), mod 64
-            const int base = select_lanes(ln.b0, ln.b1, lanes_below<SH::kP>(SH::kP - s));
-            return __int_as_float(__builtin_amdgcn_ds_permute(base + (256 + 4 * s - 4 * SH::kP), __float_as_int(v)));
-        }
-    }
-    return s == 0 ? v : bperm(rot_addr<SH>(ln, s), v);
-}
-template <class SH>
 __device__ __forceinline__ int rot_i(int v, const Lane& ln, int s)
 {
+    if constexpr (kPushRot<SH>()) {
+        if (s != 0 && (2 * SH::kP < 64 || s <= 31)) {
+            // the same rotation as a push: lane i's value goes to lane (i + s) mod P of its group.  The
+            // address is (i < P - s ? b1 : b0) + (256 + 4 s - 4 P): lane gb + i + s or gb + i + s - P, mod 64
+            int base;
+            if constexpr (SH::kMaskSelect)
+                base = select_lanes(ln.b0, ln.b1, lanes_below<SH::kP>(SH::kP - s));
+            else
+                base = (ln.i < SH::kP - s) ? ln.b1 : ln.b0;  // loop-invariant per s: hoisted by the compiler
+            return __builtin_amdgcn_ds_permute(base + (256 + 4 * s - 4 * SH::kP), v);
+        }
+    }
     return s == 0 ? v : bperm_i(rot_addr<SH>(ln, s), v);
+}
+template <class SH>
+__device__ __forceinline__ float rot(float v, const Lane& ln, int s)
+{
+    return __int_as_float(rot_i<SH>(__float_as_int(v), ln, s));
 }
 __device__ __forceinline__ int wrap(int x, int P) { return x >= P ? x - P : x; }
 
@@ -1962,12 +1970,12 @@ void bp_decode_kernel(const BpArgs a)
     const long long wave = (long long)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     const int P = SH::P(a);
     const int G = SH::kStatic ? 64 / P : a.G;
-    // with pushed rotations the one group sits on lanes [64 - P, 64); the idle lanes below it take
-    // group index 1 (never in range) and in-group indices 0 .. 63 - P (in bounds, never stored)
+    // with pushed rotations the groups sit on the top G P lanes; the idle lanes below them take group
+    // index G (never in range), in-group indices 0 .. 63 - G P (in bounds, never stored) and group 0's base
     constexpr int kGB = kGroupBase<SH>();
-    const int g = kGB ? (lane < kGB ? 1 : 0) : lane / P;
-    const int i = kGB ? (lane < kGB ? lane : lane - kGB) : lane - g * P;
-    const int gb = kGB ? kGB : g * P;
+    const int g = kGB ? (lane < kGB ? G : (lane - kGB) / P) : lane / P;
+    const int i = kGB ? (lane < kGB ? lane : lane - kGB - g * P) : lane - g * P;
+    const int gb = kGB ? (lane < kGB ? kGB : kGB + g * P) : g * P;
     // iteration-0 tables of both sectors (iteration0), built by the workgroup before any wave leaves
     constexpr int kTabX = (1 << RX) * RX, kTabZ = (1 << RZ) * RZ;
     __shared__ float tab0[QEC_TABLE0 ? kTabX + kTabZ : 1];

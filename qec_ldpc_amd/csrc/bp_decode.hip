@@ -333,6 +333,13 @@ constexpr int col_group()
 #ifndef QEC_ROT_PUSH
 #define QEC_ROT_PUSH 1
 #endif
+//   QEC_ROT_PUSH_HI  which rotations push, with the one group on lanes [64 - P, 64): 1 those with s >= P - 31
+//                    (their pulls would wrap the upper 32-lane half onto the group's first lanes, banks
+//                    shared; their pushes' destinations are distinct banks per half); 0 those with s <= 31
+//                    (the first cut).  Pulls with s <= P - 32 then read distinct banks in both halves.
+#ifndef QEC_ROT_PUSH_HI
+#define QEC_ROT_PUSH_HI 1
+#endif
 
 // The first lane of group 0 for compile-time P: with pushed rotations (QEC_ROT_PUSH) the G = 64 / P
 // groups take the top G P lanes and the 64 - G P idle lanes sit below them, else the groups start at lane 0.
@@ -627,7 +634,7 @@ template <class SH>
 __device__ __forceinline__ int rot_i(int v, const Lane& ln, int s)
 {
     if constexpr (kPushRot<SH>()) {
-        if (s != 0 && (2 * SH::kP < 64 || s <= 31)) {
+        if (s != 0 && (2 * SH::kP < 64 || (QEC_ROT_PUSH_HI ? s >= SH::kP - 31 : s <= 31))) {
             // the same rotation as a push: lane i's value goes to lane (i + s) mod P of its group.  The
             // address is (i < P - s ? b1 : b0) + (256 + 4 s - 4 P): lane gb + i + s or gb + i + s - P, mod 64
             int base;

@@ -16,8 +16,11 @@ rank 0 is timed separately, as its own component and end to end (decode + gather
 Prints one JSON line (rank 0).  Extra objects:
   roofline        the dominant kernel (the decode) against its real bound, VALU issue:
                   SQ_INSTS_VALU per launch (rocprofv3 PMC, profiles/pmc_<code>.json, per syndrome
-                  x the batch) x 2 cycles / (1024 SIMDs x 2.4 GHz x launch time), launch time
-                  from HIP events on the launch stream in this run; traffic = PMC HBM bytes.
+                  x the batch) x 2 cycles / (1024 SIMDs x 2.4 GHz x step time); step time = the GPU
+                  span per step from one HIP event pair on the launch stream around the K timed
+                  steps, so it includes any idle gap between launches (frac is then a lower bound;
+                  the rocprofv3 kernel trace under profiles/ gives the launches alone); traffic =
+                  PMC HBM bytes.
                   frac is the counter-exact figure; cost-weighted figures, the LDS issue fraction and
                   the LDS bank-conflict share sit beside it (LDS is a co-bound of the P61 kernels).
   roofline_hbm_alg  SURVEY.md 8(d)'s HBM-resident flooding-schedule bytes over the launch time:
@@ -231,8 +234,11 @@ def main():
         step = step_bits if bits else step_bytes
         # the timed step: the same call with its tensors validated once (DecoderGPU.bind), so the host
         # side of a step is the C ABI call alone
-        bound = (dec.bind(dec.decode_bits_packed_dev, sXb, sZb, p, iters, args.stop, rec, its, stream=stream) if bits
-                 else dec.bind(dec.decode_batch_packed_dev, sX, sZ, p, iters, args.stop, rec, its, stream=stream))
+        def bound_into(r):
+            return (dec.bind(dec.decode_bits_packed_dev, sXb, sZb, p, iters, args.stop, r, its, stream=stream) if bits
+                    else dec.bind(dec.decode_batch_packed_dev, sX, sZ, p, iters, args.stop, r, its, stream=stream))
+
+        bound = bound_into(rec)
     else:
         eX = torch.empty((B, code.n), dtype=torch.uint8, device=dev)
         eZ = torch.empty((B, code.n), dtype=torch.uint8, device=dev)
@@ -358,7 +364,8 @@ def main():
 
     if world > 1 and not args.no_gather and packed:
         try:
-            out["gather"] = gather_measure(dec, step, rec, B, world, rank, dev, stream, steps, global_batch, backend)
+            out["gather"] = gather_measure(dec, step, rec, B, world, rank, dev, stream, steps, global_batch, backend,
+                                           bound_into)
         except Exception as exc:  # noqa: BLE001 -- a failure here must not cost the bench line
             out["gather"] = {"error": "%s: %s" % (type(exc).__name__, exc)}
 
@@ -459,7 +466,7 @@ def timed_steps(step, steps, stream, dev, world):
 
 def valu_roofline(pm, path, B, kernel_ms):
     """VALU-issue roofline of the decode kernel: PMC SQ_INSTS_VALU (wave instructions) per
-    syndrome x B, each taking VALU_ISSUE_CYCLES of a SIMD, over this run's launch time."""
+    syndrome x B, each taking VALU_ISSUE_CYCLES of a SIMD, over this run's GPU step span (includes inter-launch gaps)."""
     peak = SIMDS * CLOCK_GHZ * 1e9 / VALU_ISSUE_CYCLES / 1e12  # T wave-instructions/s
     base = {"bound": "valu", "peak": round(peak, 4), "unit": "Twave-instr/s",
             "peak_basis": "1024 SIMDs x 2.4 GHz / 2 cycles per wave64 VALU instruction"}
@@ -585,12 +592,14 @@ def sustained(step, stream, dev, world, ms_per_step, min_seconds, per_step_units
     return {"steps": n, "seconds": round(elapsed, 3), "syndromes_per_s": round(per_step_units * n / elapsed, 1)}
 
 
-def gather_measure(dec, step, rec, B, world, rank, dev, stream, steps, global_batch, backend):
+def gather_measure(dec, step, rec, B, world, rank, dev, stream, steps, global_batch, backend, bound_into):
     """every rank's decision records (decoded straight into bit-packed form) are
-    gathered to rank 0.  Timed alone, and end to end (decode + gather each step)."""
+    gathered to rank 0.  Timed alone, end to end serialised (decode, then gather, each step), and end to
+    end overlapped (qec_ldpc_amd.gather.GatherPipeline: step k + 1 decodes into a second record buffer
+    while step k's records are gathered on a communication stream, events only)."""
     import torch
     import torch.distributed as dist
-    from qec_ldpc_amd.gather import gather_records
+    from qec_ldpc_amd.gather import GatherPipeline, gather_records
     gather_records(rec)  # warm-up (communicator set-up)
     torch.cuda.synchronize(dev)
 
@@ -615,9 +624,20 @@ def gather_measure(dec, step, rec, B, world, rank, dev, stream, steps, global_ba
     ok = True
     if rank == 0:
         ok = bool(torch.equal(full[:B], rec))
-    t = torch.tensor([g, e], dtype=torch.float64, device=dev)
+    pipe = GatherPipeline(tuple(rec.shape), dev)
+    calls = [bound_into(pipe.bufs[0]), bound_into(pipe.bufs[1])]
+
+    def decode(k, r, s):
+        calls[k % 2]()
+
+    pipe.run(decode, 2)  # warm-up
+    o = timed(lambda: pipe.run(decode, steps), 1) / steps
+    ok_o = True
+    if rank == 0:  # every step decodes the same shard: the last gathered batch starts with rank 0's records
+        ok_o = bool(torch.equal(pipe.outs[(steps - 1) % 2][:B].to(rec.device), rec))
+    t = torch.tensor([g, e, o], dtype=torch.float64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    g, e = float(t[0]), float(t[1])
+    g, e, o = float(t[0]), float(t[1]), float(t[2])
     nbytes = B * rec.shape[1]
     coll = "RCCL" if backend == "nccl" else backend
     rccl = None
@@ -632,6 +652,13 @@ def gather_measure(dec, step, rec, B, world, rank, dev, stream, steps, global_ba
             "gather_ms": round(g * 1e3, 4), "root_GBps": round(world * nbytes / g / 1e9, 2),
             "end_to_end": {"ms_per_step": round(e * 1e3, 4), "syndromes_per_s": round(global_batch / e, 1),
                            "what": "packed decode of every shard + %s gather of all records to rank 0" % coll},
+            "end_to_end_overlapped": {
+                "ms_per_step": round(o * 1e3, 4), "syndromes_per_s": round(global_batch / o, 1),
+                "gather_bytes_per_step": int(world * nbytes),
+                "what": "packed decode of step k + 1 overlapped with the %s gather of step k's records to rank 0 "
+                        "(two record buffers, a communication stream, events only; qec_ldpc_amd.gather."
+                        "GatherPipeline)" % coll,
+                "rank0_last_step_intact": ok_o},
             "rank0_shard_intact": ok}
 
 

@@ -35,6 +35,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <type_traits>
 
 #include "qec_device.h"
 #include "qec_internal.h"
@@ -1868,6 +1869,25 @@ __device__ __forceinline__ void decode_sector(const BpArgs& a, Lane& ln, uint32_
     }
 }
 
+// The syndrome stop without the hard-message forms: every iteration in soft arithmetic (bit-identical:
+// the forms are exact shortcuts).  Under the syndrome stop a sector that turns hard has in practice
+// satisfied its syndrome already (P61 at p = 0.02 .. 0.1: no hard iteration among 16 384 syndromes,
+// tools/kbench/phase_hist.py, profiles/r06/phase_hist.txt), so tracking the hard state -- an fma and an
+// OR per outgoing message and a compare per column in every soft var pass, ~10 % of a P61 soft iteration
+// -- and the hard branches' registers are pure cost there.
+//   QEC_SYN_HARD  1: the syndrome-stop kernels keep the hard-message forms (the round-5 kernels)
+#ifndef QEC_SYN_HARD
+#define QEC_SYN_HARD 0
+#endif
+template <class TU>
+struct SoftTune : TU {
+    static constexpr bool kSaturate = false;
+};
+// Taken for one-group waves (P61); P7's syndrome-stop kernels (nine groups per wave) keep the forms.
+template <int STOP, class SH, class TU>
+using StopTune = typename std::conditional<STOP == QEC_STOP_SYNDROME && !QEC_SYN_HARD && SH::kStatic && (2 * SH::kP > 64),
+                                           SoftTune<TU>, TU>::type;
+
 // Tuning knobs (compile-time; tools/kbench/ sweeps them).
 #ifndef QEC_WAVES_PER_BLOCK
 #define QEC_WAVES_PER_BLOCK 0   // 0: per-variant (Tune<>::kWavesPerBlock)
@@ -2026,7 +2046,7 @@ void bp_decode_kernel(const BpArgs a)
                 // be hoisted out of this loop into live registers (they spilled at 3 waves per SIMD)
                 int il = i, gbl = gb;
                 asm volatile("" : "+v"(il), "+v"(gbl));
-                decode_group<RX, RZ, L, STOP, SH, TU, MODE>(a, tab0, stage, il, gbl, b, in_range, doX);
+                decode_group<RX, RZ, L, STOP, SH, StopTune<STOP, SH, TU>, MODE>(a, tab0, stage, il, gbl, b, in_range, doX);
             }
             return;
         }
@@ -2051,7 +2071,7 @@ void bp_decode_kernel(const BpArgs a)
             bool dX2, ir2;
             const uint32_t b2 = entry(vw + 2 * nw, dX2, ir2);
             const uint32_t sb1 = vw + nw < wTot ? bits(b1, dX1, ir1) : 0u;
-            decode_group<RX, RZ, L, STOP, SH, TU, MODE>(a, tab0, stage, i, gb, b0, ir0, dX0, true, sb0);
+            decode_group<RX, RZ, L, STOP, SH, StopTune<STOP, SH, TU>, MODE>(a, tab0, stage, i, gb, b0, ir0, dX0, true, sb0);
             b0 = b1; dX0 = dX1; ir0 = ir1; sb0 = sb1;
             b1 = b2; dX1 = dX2; ir1 = ir2;
         }
@@ -2066,7 +2086,7 @@ void bp_decode_kernel(const BpArgs a)
     const bool doX = MODE == 3 || (MODE != 4 && (!SPLIT || (wave & 1) == 0));  // wave-uniform
     const long long pslot = (a.perm_sectors && !doX) ? slot + a.B : slot;
     const uint32_t b = (in_range && a.perm != nullptr) ? (uint32_t)a.perm[pslot] : (uint32_t)slot;
-    decode_group<RX, RZ, L, STOP, SH, TU, MODE>(a, tab0, stage, i, gb, b, in_range, doX);
+    decode_group<RX, RZ, L, STOP, SH, StopTune<STOP, SH, TU>, MODE>(a, tab0, stage, i, gb, b, in_range, doX);
 }
 
 // ---- variant table ----------------------------------------------------------

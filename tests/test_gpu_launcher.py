@@ -50,6 +50,9 @@ def test_bench_two_ranks():
     assert g["backend"] == "gloo" and g["backend_reported"] == "gloo" and g["world_size"] == 2
     assert g["rank0_shard_intact"] is True
     assert "gloo gather" in g["end_to_end"]["what"]
+    o = g["end_to_end_overlapped"]
+    assert o["rank0_last_step_intact"] is True and o["syndromes_per_s"] > 0
+    assert o["gather_bytes_per_step"] == 16384 * g["record_bytes"]
     assert b["full_arithmetic"]["identical"] is True and b["ref_stop"]["syndromes_per_s"] > 0
     assert 0 < b["executed_iteration_fraction"] <= 1
 

@@ -4,7 +4,8 @@ allows one rank per GPU, and the box has one).  In a child process, so the proce
 outlives the test:
 
 * gather_records' RCCL branch: a real dist.gather of device-resident decision records into the
-  root's output (qec_ldpc_amd/gather.py), byte-equal to what was decoded;
+  root's output (qec_ldpc_amd/gather.py), byte-equal to what was decoded; and the overlapped
+  decode + gather pipeline (GatherPipeline) over three steps, every gathered step byte-equal;
 * tools/psweep.py's counter reduction: the all-reduce (sum) of the counter vector and the
   all-reduce (max) of the timings on device tensors, on a real Monte-Carlo run's counters.
 
@@ -49,11 +50,18 @@ its = torch.empty((B, 2), dtype=torch.int32, device=dev)
 dec.decode_batch_packed_dev(sX, sZ, 0.01, 50, "fixed", rec, its, stream=st)
 full = gather_records(rec)
 torch.cuda.synchronize()
+from qec_ldpc_amd.gather import GatherPipeline
+pipe = GatherPipeline(tuple(rec.shape), dev)
+piped = []
+pipe.run(lambda k, r, s: dec.decode_batch_packed_dev(sX, sZ, 0.01, 50, "fixed", r, its, stream=s), 3,
+         sink=lambda k, o: piped.append(o.clone()))
 r = dec.monte_carlo(0x51EC0DE, 0, 8192, 0.01, 50, "syndrome", 8192)
 c, tm = psweep.reduce_counters(r, [0.5, 0.25, 0.1, 0.9, 0.0], "nccl", dev)
 out = {"backend": dist.get_backend(), "world": dist.get_world_size(),
        "gather_device": str(full.device), "gather_equal": bool(full is not rec and torch.equal(full, rec)),
        "gather_shape": list(full.shape),
+       "pipeline_equal": len(piped) == 3 and all(torch.equal(x, rec) for x in piped),
+       "pipeline_device": str(pipe.outs[0].device),
        "counters_equal": all(c[k] == r[k] for k in psweep.FIELDS), "tested": c["tested"], "times": tm}
 dist.barrier()
 dist.destroy_process_group()
@@ -74,5 +82,6 @@ def test_rccl_gather_and_counter_reduce_world1():
     out = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
     assert out["backend"] == "nccl" and out["world"] == 1
     assert out["gather_equal"] and out["gather_device"] == "cuda:0" and out["gather_shape"][0] == 4096
+    assert out["pipeline_equal"] and out["pipeline_device"] == "cuda:0"
     assert out["counters_equal"] and out["tested"] == 8192
     assert out["times"] == [0.5, 0.25, 0.1, 0.9, 0.0]

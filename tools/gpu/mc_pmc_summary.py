@@ -1,5 +1,6 @@
 """Reduce one p of tools/gpu/run_mc_profile.sh (a kernel-trace pass and five PMC passes of
-`tools/psweep.py --ps P --reps 1`: 2^20 samples in one batch) into profiles/pmc_mc_p61_p<P>.json, which
+`tools/psweep.py --stop S --ps P --reps 1`: 2^20 samples in one batch) into profiles/pmc_mc_p61_p<P>.json
+(syndrome stop) or profiles/pmc_mc_p61_<S>_p<P>.json (other stop rules), which
 tools/psweep.py reads for the roofline of its lines.
 
 Per kernel of the Monte-Carlo call (fused sampler/triage kernel, list-mode decode, survivor statistics,
@@ -35,6 +36,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--dir", required=True)
     ap.add_argument("--p", type=float, required=True)
+    ap.add_argument("--stop", default="syndrome", choices=["syndrome", "fixed", "ref"])
     ap.add_argument("--out", required=True)
     a = ap.parse_args()
     durs = {}
@@ -56,9 +58,10 @@ def main():
     root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     sys.path.insert(0, root)
     import qec_ldpc_amd
-    out = {"p": a.p, "samples": 1 << 20, "batch": 1 << 20, "stop": "syndrome", "iters": 50,
+    out = {"p": a.p, "samples": 1 << 20, "batch": 1 << 20, "stop": a.stop, "iters": 50,
            "code": "J_4_K_5_L_10_P_61_s_9_t_49", "build_id": qec_ldpc_amd.build_id(),
-           "source": "tools/gpu/run_mc_profile.sh (rocprofv3 kernel trace + 5 PMC passes of tools/psweep.py --ps P --reps 1)",
+           "source": "tools/gpu/run_mc_profile.sh (rocprofv3 kernel trace + 5 PMC passes of tools/psweep.py --stop %s "
+                     "--ps P --reps 1)" % a.stop,
            "kernels": {}}
     for k, d in sorted(durs.items()):
         if k.startswith("__amd_rocclr"):

@@ -18,9 +18,15 @@ def main():
         vg = re.search(r"\.amdhsa_next_free_vgpr (\d+)", meta).group(1)
         n = len(re.findall(r"^\s+[vsdgb][a-z_0-9]+ ", body, re.M))
         short = re.sub(r"GeneratedShifts<.*", "", name)
-        print("%-60s %-8s instrs %6d vgpr %4s bperm %4d scratch %d" % (
-            name[:60], "split" if name.endswith("Lb1EEEvNS_6BpArgsE") else "", n, vg, body.count("ds_bpermute"),
-            body.count("scratch_")))
+        rx = re.match(r"_ZN3qec16bp_decode_kernelILi(\d+)ELi(\d+)ELi(\d+)ELi(\d)", name)
+        tune = re.search(r"(SeqSynTune|ListTune|MinReg|Phase|RuntimeShifts)", name)
+        mode = re.search(r"ELi(\d)EEEvNS_6BpArgsE$", name)
+        stopn = {"0": "ref", "1": "fixed", "2": "syn"}[rx.group(4)] if rx else "?"
+        sc = re.search(r"ScratchSize: (\d+)", meta)
+        print("J%s K%s L%s %-5s mode %s %-13s instrs %6d vgpr %4s bperm %4d scratch-instrs %d scratch %s B" % (
+            rx.group(1) if rx else "?", rx.group(2) if rx else "?", rx.group(3) if rx else "?", stopn,
+            mode.group(1) if mode else "?", tune.group(1) if tune else "", n, vg, body.count("ds_bpermute"),
+            body.count("scratch_"), sc.group(1) if sc else "?"))
 
 
 if __name__ == "__main__":

@@ -40,12 +40,14 @@ def summarize(p, c, seconds, world):
 
 
 def mc_roofline(p, samples, stop, iters, batch, code_name):
-    """The roofline of a sweep point from its rocprofv3 profile (profiles/pmc_mc_p61_p<p>.json,
+    """The roofline of a sweep point from its rocprofv3 profile (profiles/pmc_mc_p61_p<p>.json; other stop
+    rules than the syndrome stop pmc_mc_p61_<stop>_p<p>.json;
     tools/gpu/run_mc_profile.sh): per kernel its dispatch time and VALU / LDS issue fractions, and the
     dominant kernel's bound -- only from a profile of this workload (p, samples, batch, stop, cap) taken
     on this very build of the library (else the reason)."""
     import qec_ldpc_amd as q
-    path = os.path.join(ROOT, "profiles", "pmc_mc_p61_p%g.json" % p)
+    sfx = "" if stop == "syndrome" else stop + "_"
+    path = os.path.join(ROOT, "profiles", "pmc_mc_p61_%sp%g.json" % (sfx, p))
     try:
         with open(path) as f:
             pm = json.load(f)

@@ -146,7 +146,14 @@ int main(int argc, char** argv)
         int w, W, COUNT, MAX_ITERATIONS;
         float p;
         init >> w >> W >> COUNT >> MAX_ITERATIONS >> p;
+        const bool read_ok = !init.fail();
         init.close();
+        if (!read_ok || COUNT < 0 || MAX_ITERATIONS < 0) {
+            // main.cu:74-88 reads the same fields; a negative or unread COUNT would wrap to ~1.8e19 samples
+            // in the Philox run below (main.cu's own loop just does nothing then)
+            std::cerr << initFile << ": expected 'codeFile w W COUNT MAX p' with COUNT >= 0 and MAX >= 0" << std::endl;
+            return 2;
+        }
         if (rng == "philox") {
             DecoderGPU decoder(code, devices);
             std::cout << "Engine: " << decoder.Describe() << std::endl;

@@ -44,273 +44,58 @@
 
 namespace qec {
 
-// Design options.  Each kernel variant carries its own measured choice of RELABEL, MASK_SELECT,
-// PIPELINE, FASTDIV, ZEROSKIP and SATURATE (Tune<> in the variant table below); defining one of
-// those macros overrides it for every variant.  The rest are global experiment switches.
-// tools/kbench sweeps them.
-//   QEC_RELABEL      spanning-tree lane relabelling (fewer ds_bpermute, but more distinct shifts)
-//   QEC_MASK_SELECT  rotation base chosen by a constant lane mask instead of hoisted addresses
-#ifndef QEC_RELABEL
-#define QEC_RELABEL -1
-#endif
-#ifndef QEC_MASK_SELECT
-#define QEC_MASK_SELECT -1
-#endif
-//   QEC_PIPELINE     D: keep the gathers of the next D columns in flight during a column's arithmetic
-#ifndef QEC_PIPELINE
-#define QEC_PIPELINE -1
-#endif
-//   QEC_FASTDIV      guarded short division (see div_short below)
-#ifndef QEC_FASTDIV
-#define QEC_FASTDIV -1
-#endif
-//   QEC_GUARD_MIN    1: the short-division guard of a column as two min-reductions
-#ifndef QEC_GUARD_MIN
-#define QEC_GUARD_MIN 1
-#endif
-//   QEC_GUARD_ZERO   1: the division guard only excludes numerators in (0, 2^-98) when p' <= 1/2
-//                    (zero_ok); 0: the general guard (numerators and denominators)
-#ifndef QEC_GUARD_ZERO
-#define QEC_GUARD_ZERO 1
-#endif
-//   QEC_GUARD_GLOBAL 1: one bound per soft var pass (short_domain) selects a guard-free pass
-#ifndef QEC_GUARD_GLOBAL
-#define QEC_GUARD_GLOBAL 0
-#endif
-//   QEC_ZEROSKIP     a column whose every numerator is +0 (and denominator > 0) on every live
-//                    lane gets q = +0 without dividing (IEEE: +0 / d = +0 for d > 0)
-#ifndef QEC_ZEROSKIP
-#define QEC_ZEROSKIP -1
-#endif
-//   QEC_SATURATE     hard-message fast paths once every message of a sector is exactly 0 or 1
-//                    (see check_pass_hard / var_pass below)
-#ifndef QEC_SATURATE
-#define QEC_SATURATE -1
-#endif
-//   QEC_AGREE        0: hard sectors skip the whole-sector agreement test (var_pass_agree)
-#ifndef QEC_AGREE
-#define QEC_AGREE 1
-#endif
-//   QEC_PHASE_STATS  experiment builds only: iters[] reports, per sector, the iterations spent in
-//                    each phase (soft | hard << 8 | agreed << 16 | jumped << 24) instead of the count
+// Design choices.  Every one below was measured on the chip and is fixed; the measurements of the
+// alternatives (and the build flags that selected them, removed in round 6) are in profiles/r0*/ and
+// DESIGN.md's changelog.  Each kernel variant carries its own measured choice of lane relabelling,
+// mask-selected rotation bases, gather pipelining, short division, zero-skip, hard-message forms and
+// occupancy (Tune<> in the variant table below).
+//   QEC_PHASE_STATS  instrumented kernels only (bp_decode_phase.hip, QEC_OPT_PHASE_STATS): iters[] reports,
+//                    per sector, the iterations spent in each phase (soft | hard << 8 | agreed << 16 |
+//                    jumped << 24) instead of the count.  The Makefile builds both states.
 #ifndef QEC_PHASE_STATS
 #define QEC_PHASE_STATS 0
 #endif
-//   QEC_ABLATE       timing experiments only (wrong outputs): 1 = skip the post-processing
-#ifndef QEC_ABLATE
-#define QEC_ABLATE 0
-#endif
-//   QEC_TABLE0       iteration 0 from a per-workgroup table (iteration0)
-#ifndef QEC_TABLE0
-#define QEC_TABLE0 1
-#endif
-//   QEC_ZERO_SYNDROME  syndrome stop: a sector whose syndrome is zero on every live lane of the wave
-//                      skips to its known outputs (decode_sector)
-#ifndef QEC_ZERO_SYNDROME
-#define QEC_ZERO_SYNDROME 1
-#endif
-//   QEC_ZERO_OUTCOME fixed / reference stop: a wave whose sector syndromes are all zero takes the launch's
-//                    precomputed zero-syndrome outcome (zero_outcome) instead of iterating
-#ifndef QEC_ZERO_OUTCOME
-#define QEC_ZERO_OUTCOME 1
-#endif
-//   QEC_SYN_EARLY    syndrome stop: iteration 0 tests the syndrome before forming its messages
-#ifndef QEC_SYN_EARLY
-#define QEC_SYN_EARLY 1
-#endif
-//   QEC_TABLE0_HOST  the iteration-0 tables come from the host through the kernel arguments instead
-//                    of being computed by every workgroup (~10 % of a low-p syndrome-stop launch)
-#ifndef QEC_TABLE0_HOST
-#define QEC_TABLE0_HOST 1
-#endif
-//   QEC_TRACK_FROM   first iteration whose var pass tests whether the sector became hard
-#ifndef QEC_TRACK_FROM
-#define QEC_TRACK_FROM 2
-#endif
-//   QEC_LONG_PRIO    n > 0: a sector still running at iteration n (almost every sector has jumped
-//                    to its end by iteration 7) raises its wave's issue priority, so the few
-//                    never-hardening waves, which set the launch's tail, lose less time to the
-//                    waves sharing their SIMD (0: off; no effect beyond noise at n = 5..20:
-//                    profiles/r01/session7/cmp_s7d_*.txt -- those waves are latency-bound, not
-//                    starved of issue slots)
-#ifndef QEC_LONG_PRIO
-#define QEC_LONG_PRIO 0
-#endif
-//   (a row-by-row XOR form for rows that harden before their sector, QEC_ROW_HARD, was measured
-//    slower in round 1 -- rows rarely harden before their whole sector does -- and removed)
-//   QEC_SYN_ROWBARRIER  the syndrome test of the syndrome stop rule rotates one row at a time
-#ifndef QEC_SYN_ROWBARRIER
-#define QEC_SYN_ROWBARRIER 1
-#endif
-//   QEC_AGREE_SYN    the syndrome-stop kernels take the agreement test too (kAgree)
-#ifndef QEC_AGREE_SYN
-#define QEC_AGREE_SYN 0
-#endif
-//   QEC_SYN_RELAUNDER   the syndrome test recomputes its rotation addresses (see iteration)
-#ifndef QEC_SYN_RELAUNDER
-#define QEC_SYN_RELAUNDER 1
-#endif
-//   QEC_SYN_SKIP_SEEN  syndrome stop: an iteration whose hard decision equals (group-wide) one of the two
-//                      last tested ones -- both failed, or the group would have stopped -- skips the test
-#ifndef QEC_SYN_SKIP_SEEN
-#define QEC_SYN_SKIP_SEEN 1
-#endif
-//   QEC_SYN_BALLOT   compile-time shifts: syndrome tests from ballots and scalar rotations (group_syndrome_ok)
-#ifndef QEC_SYN_BALLOT
-#define QEC_SYN_BALLOT 0
-#endif
-//   QEC_SYN_ROW0_FIRST  syndrome stop: test row 0 (lane-local with the relabelled tables) before the others
-#ifndef QEC_SYN_ROW0_FIRST
-#define QEC_SYN_ROW0_FIRST 1
-#endif
-//   QEC_IDENT_AGREE  a hard var pass whose every column took the agreeing-inputs shortcut counts as the
-//                    agreement path (the cycle jump's entry) where var_pass_agree is not run
-#ifndef QEC_IDENT_AGREE
-#define QEC_IDENT_AGREE 0
-#endif
-//   QEC_SYN_DEFER_RETURN  syndrome stop, one group per wave: a var pass leaves its outputs in the variable view
-//                         and rotates them back to the check view only when the sector goes on (defer_return)
-#ifndef QEC_SYN_DEFER_RETURN
-#define QEC_SYN_DEFER_RETURN 1
-#endif
-//   QEC_SCALED_DIV   var passes with at most 4 factors per fold divide guard-free on 2^32-scaled folds
-#ifndef QEC_SCALED_DIV
-#define QEC_SCALED_DIV 1
-#endif
-//   QEC_ASSUME_SCALED  experiment: the scaled short division without the launch-wide test (kernels then
-//                      valid only for p' in [2^-20, 1/2]); straight-line soft var passes, but the P61 fixed /
-//                      reference kernels then spill 40-44 B: headline +3.6 %, full arithmetic -4 %
-//                      (profiles/r03/cmp_assume_scaled_p61.txt) -- not taken
-#ifndef QEC_ASSUME_SCALED
-#define QEC_ASSUME_SCALED 0
-#endif
-//   QEC_COL_BARRIER  a scheduling barrier after each column group of a var pass: the machine scheduler
-//                    otherwise hoists work across columns into more live registers; P61 headline +2.8 %
-//                    (+7.2 % on another box), full arithmetic +0.9 %, P7 and the other stop rules neutral
-//                    (profiles/r03/cmp_col_barrier_*.txt)
-#ifndef QEC_COL_BARRIER
-#define QEC_COL_BARRIER 1
-#endif
-//   QEC_ROW_BARRIER  -1 per variant (Tune::kRowBarrier), 0 / 1 force: a scheduling barrier after each
-//                    check-pass row.  P61 headline +2.3 % in one A/B, -0.6 % in the next (noise), full
-//                    arithmetic -1.2 %; P7 -1..-3 % (profiles/r03/cmp_row_barrier_*.txt): off everywhere
-#ifndef QEC_ROW_BARRIER
-#define QEC_ROW_BARRIER -1
-#endif
-//   QEC_SOFT_STRAIGHT  soft var passes: 1 no per-column agreement branch (P61 headline +3.6 %, P7 +1 %),
-//                      2 also one division branch per pass (two copies of each var pass in the loop: P61 2x
-//                      slower, P7 -3 %; profiles/r03/cmp_soft_straight_*.txt)
-#ifndef QEC_SOFT_STRAIGHT
-#define QEC_SOFT_STRAIGHT 1
-#endif
-//   QEC_COL_GROUP    columns per division guard in soft var passes (var_pass); 0: per variant
-#ifndef QEC_COL_GROUP
-#define QEC_COL_GROUP 0
-#endif
-#define QEC_PICK(macro, dflt) ((macro) >= 0 ? (macro) != 0 : (dflt))
-//   QEC_LIST_STAMPS  experiment builds only: syndrome-stop sectors add s_memtime phase spans (cycles) and
-//                    counts to g_list_stamps (read by qec_debug_list_stamps, tools/kbench/list_stamps.py)
-#ifndef QEC_LIST_STAMPS
-#define QEC_LIST_STAMPS 0
-#endif
+// First iteration whose var pass tests whether the sector became hard (iterations 0 and 1 essentially
+// never end hard; skipping the test there only delays the exact hard forms, never changes a bit).
+constexpr int kTrackFrom = 2;
 
 // Per-variant tuning: minimum waves per SIMD for the register allocator, and the options above.
-//   QEC_SEQ_MINW_X / _Z  experiment: min waves per SIMD of the sector-launch kernels (MODE 3 / 4), all variants
-#ifndef QEC_SEQ_MINW_X
-#define QEC_SEQ_MINW_X 0
-#endif
-#ifndef QEC_SEQ_MINW_Z
-#define QEC_SEQ_MINW_Z 0
-#endif
 template <int MINW_, bool RELABEL_, bool ZEROSKIP_, bool FASTDIV_, bool SATURATE_ = false, bool SPLIT_ = false,
           bool MASKSEL_ = false, int PIPE_ = 0, int WPB_ = 4, int SYNW_ = 0, int CG_ = 1, bool ROWB_ = false,
           int MWX_ = 0, int MWZ_ = 0>
 struct Tune {
     // sector launches (MODE 3 / 4: one kernel per sector, each compiled for its own sector only): their
     // occupancy, 0 = kMinWaves
-    static constexpr int kMinWavesX = QEC_SEQ_MINW_X > 0 ? QEC_SEQ_MINW_X : MWX_ > 0 ? MWX_ : MINW_;
-    static constexpr int kMinWavesZ = QEC_SEQ_MINW_Z > 0 ? QEC_SEQ_MINW_Z : MWZ_ > 0 ? MWZ_ : MINW_;
-    static constexpr bool kRowBarrier = QEC_PICK(QEC_ROW_BARRIER, ROWB_);
-    static constexpr int kColGroup = QEC_COL_GROUP > 0 ? QEC_COL_GROUP : CG_;  // columns per division guard
+    static constexpr int kMinWavesX = MWX_ > 0 ? MWX_ : MINW_;
+    static constexpr int kMinWavesZ = MWZ_ > 0 ? MWZ_ : MINW_;
+    static constexpr bool kRowBarrier = ROWB_;  // a scheduling barrier after each check-pass row
+    static constexpr int kColGroup = CG_;       // columns per division guard in soft var passes
     static constexpr int kMinWaves = MINW_;
     static constexpr int kMinWavesSyn = SYNW_ > 0 ? SYNW_ : MINW_;  // the syndrome-stop kernels
-    static constexpr int kWavesPerBlock = WPB_;  // waves per workgroup (QEC_WAVES_PER_BLOCK overrides)
-    static constexpr bool kMaskSelect = QEC_PICK(QEC_MASK_SELECT, MASKSEL_);
-    static constexpr int kPipeline = QEC_PIPELINE >= 0 ? QEC_PIPELINE : PIPE_;
+    static constexpr int kWavesPerBlock = WPB_;  // waves per workgroup
+    static constexpr bool kMaskSelect = MASKSEL_;  // rotation base chosen by a constant lane mask (rot_addr)
+    static constexpr int kPipeline = PIPE_;  // D: the gathers of the next D columns in flight during a column
     static constexpr bool kSplit = SPLIT_;  // QEC_OPT_SECTOR_SPLIT = 1 (auto) splits sectors for this variant
-    static constexpr bool kRelabel = QEC_PICK(QEC_RELABEL, RELABEL_);
-    static constexpr bool kZeroSkip = QEC_PICK(QEC_ZEROSKIP, ZEROSKIP_);
-    static constexpr bool kFastDiv = QEC_PICK(QEC_FASTDIV, FASTDIV_);
-    static constexpr bool kSaturate = QEC_PICK(QEC_SATURATE, SATURATE_);
-    static constexpr bool kAgreeSyn = false;  // the syndrome stop takes the agreement test (kAgree)
+    static constexpr bool kRelabel = RELABEL_;  // spanning-tree lane relabelling (relabel below)
+    static constexpr bool kZeroSkip = ZEROSKIP_;  // a column of +0 numerators skips its divisions
+    static constexpr bool kFastDiv = FASTDIV_;  // the short division (div_short)
+    static constexpr bool kSaturate = SATURATE_;  // the hard-message forms (check_pass_hard, var_pass)
+    static constexpr bool kAgreeSyn = false;  // the syndrome stop takes the agreement test (kAgree): never
     static constexpr int kSeqSynWavesX = kMinWavesSyn, kSeqSynWavesZ = kMinWavesSyn;  // sector launches, syndrome stop
 };
 
-//   QEC_SEQ_AGREE_SYN        the syndrome-stop sector launches (MODE 3 / 4) take the agreement test and the
-//                            cycle jump (SeqSynTune), at their own occupancy (QEC_SEQ_SYN_MINW_X / _Z)
-#ifndef QEC_SEQ_AGREE_SYN
-#define QEC_SEQ_AGREE_SYN 0
-#endif
-#ifndef QEC_SEQ_SYN_MINW_X
-#define QEC_SEQ_SYN_MINW_X 5
-#endif
-#ifndef QEC_SEQ_SYN_MINW_Z
-#define QEC_SEQ_SYN_MINW_Z 0
-#endif
-//   QEC_SEQ_SYN_MINREG       the P61 syndrome-stop sector launches from the minreg unit (bp_decode_p61.hip)
-#ifndef QEC_SEQ_SYN_MINREG
-#define QEC_SEQ_SYN_MINREG 0
-#endif
-// The syndrome-stop sector launches of a variant: with the agreement test a sector that never satisfies
-// its syndrome jumps to its cap once its hard state cycles, instead of running every hard iteration (the
-// one-wave-per-syndrome kernels leave the test out to stay spill-free; a kernel compiled for one sector
-// has the registers for it at three waves per SIMD).
+// The syndrome-stop sector launches of a variant: X at five waves per SIMD where the variant's syndrome
+// kernels take fewer (P61: 4 -> 5, +2 %; higher occupancies spill and lose 15-40 %,
+// profiles/r06/ab/cmp_occupancy_r06c.txt); Z at the variant's own.
 template <class TU>
 struct SeqSynTune : TU {
-    static constexpr bool kAgreeSyn = QEC_SEQ_AGREE_SYN != 0;
-    // the overrides only raise a variant's occupancy (P61 X: 4 -> 5 waves; P7 keeps its 7)
-    static constexpr int kSeqSynWavesX = QEC_SEQ_SYN_MINW_X > TU::kMinWavesSyn ? QEC_SEQ_SYN_MINW_X : TU::kMinWavesSyn;
-    static constexpr int kSeqSynWavesZ = QEC_SEQ_SYN_MINW_Z > TU::kMinWavesSyn ? QEC_SEQ_SYN_MINW_Z : TU::kMinWavesSyn;
+    static constexpr int kSeqSynWavesX = 5 > TU::kMinWavesSyn ? 5 : TU::kMinWavesSyn;
 };
 
-//   QEC_LIST_MINW_P61 / _P7   min waves per SIMD of the list-mode kernels (ListTune); QEC_LIST_AGREE 0: no
-//                             agreement test / cycle jump there
-#ifndef QEC_LIST_AGREE
-#define QEC_LIST_AGREE 0
-#endif
-//   QEC_LIST_PREFETCH      list mode: the next sector's list entry and syndrome bits loaded ahead (measured:
-//                          no gain at p = 2e-3 / 5e-3, -3 % at 1e-2; off)
-//   QEC_LIST_MERGE_ONLY    list mode of the fused Monte-Carlo pipeline: flags into the merge word only
-#ifndef QEC_LIST_PREFETCH
-#define QEC_LIST_PREFETCH 0
-#endif
-#ifndef QEC_LIST_MERGE_ONLY
-#define QEC_LIST_MERGE_ONLY 1
-#endif
-//   QEC_LIST_SECTORS       list mode as two launches, one kernel per sector (MODE 5 / 6), each compiled
-//                          (and its registers allocated) for its own sector, instead of one kernel for both
-//   QEC_LIST_GO            list mode skips iteration 0's syndrome test (the triage listed the sector because it fails)
-#ifndef QEC_LIST_GO
-#define QEC_LIST_GO 1
-#endif
-#ifndef QEC_LIST_SECTORS
-#define QEC_LIST_SECTORS 0
-#endif
-//   QEC_LIST_MINW_X / _Z   experiment: min waves per SIMD of the per-sector list kernels (all variants)
-#ifndef QEC_LIST_MINW_X
-#define QEC_LIST_MINW_X 0
-#endif
-#ifndef QEC_LIST_MINW_Z
-#define QEC_LIST_MINW_Z 0
-#endif
-// The list-mode (MODE 2, or per sector MODE 5 / 6) tuning of a variant: its own occupancies and the
-// agreement test with the cycle jump under the syndrome stop (see kAgree).
-template <class TU, int LW, int LWX = 0, int LWZ = 0>
+// The list-mode (MODE 2) tuning of a variant: its own occupancy (no agreement test, no cycle jump).
+template <class TU, int LW>
 struct ListTune : TU {
     static constexpr int kMinWavesSyn = LW;
-    static constexpr int kListMinWavesX = QEC_LIST_MINW_X > 0 ? QEC_LIST_MINW_X : LWX > 0 ? LWX : LW;
-    static constexpr int kListMinWavesZ = QEC_LIST_MINW_Z > 0 ? QEC_LIST_MINW_Z : LWZ > 0 ? LWZ : LW;
-    static constexpr bool kAgreeSyn = QEC_LIST_AGREE != 0;
 };
 
 // the largest divisor of L not above the variant's column-group size
@@ -322,41 +107,32 @@ constexpr int col_group()
     return g;
 }
 
-//   QEC_ROT_PUSH   one-group waves (32 < P < 64): a rotation whose pull wraps inside a 32-lane half
-//                  (source lane i - s + P for i < s, with s <= 31) is made as the same rotation pushed
-//                  instead (ds_permute_b32, lane i to lane i + s mod P).  A wrapping ds_bpermute puts two
-//                  sources of its first half on one LDS bank and costs 7.1 instead of 6.1 cycles; a push
-//                  of any shift costs 6.1 (tools/kbench/perm_probe.hip, profiles/r05/perm_probe.txt).  The
-//                  group then sits on the TOP P lanes of the wave, [64 - P, 64), and the 64 - P idle lanes
-//                  below it: when several lanes push to one lane the highest-numbered source wins (the ISA's
-//                  DS_PERMUTE_B32 rule; tools/kbench/permute_collide.hip checks it on the chip), so an idle
-//                  lane's push never overwrites a group lane's (the group's pushes are a bijection on it).
-#ifndef QEC_ROT_PUSH
-#define QEC_ROT_PUSH 1
-#endif
-//   QEC_ROT_PUSH_HI  which rotations push, with the one group on lanes [64 - P, 64): 1 those with s >= P - 31
-//                    (their pulls would wrap the upper 32-lane half onto the group's first lanes, banks
-//                    shared; their pushes' destinations are distinct banks per half); 0 those with s <= 31
-//                    (the first cut).  Pulls with s <= P - 32 then read distinct banks in both halves.
-#ifndef QEC_ROT_PUSH_HI
-#define QEC_ROT_PUSH_HI 1
-#endif
+// Rotations by push, one-group waves (32 < P < 64): a rotation whose pull would wrap a 32-lane half
+// (source lane i - s + P for i < s) is made as the same rotation pushed instead (ds_permute_b32, lane i to
+// lane i + s mod P).  A wrapping ds_bpermute puts two sources of one half on one LDS bank and costs 7.1
+// instead of 6.1 cycles; a push of any shift costs 6.1 (tools/kbench/perm_probe.hip,
+// profiles/r05/perm_probe.txt).  The group then sits on the TOP P lanes of the wave, [64 - P, 64), and
+// the 64 - P idle lanes below it: when several lanes push to one lane the highest-numbered source wins
+// (the ISA's DS_PERMUTE_B32 rule; tools/kbench/permute_collide.hip checks it on the chip), so an idle
+// lane's push never overwrites a group lane's (the group's pushes are a bijection on it).  With the group
+// on lanes [64 - P, 64) the rotations with s >= P - 31 push (their pulls would wrap the upper half onto
+// the group's first lanes, banks shared; their pushes' destinations are distinct banks per half) and pulls
+// with s <= P - 32 read distinct banks in both halves.  Multi-group waves (P7) keep their pulls (pushing
+// every shift measured -1.8 .. +0.5 %, profiles/r05/cmp_rot_push.txt).
 
-// The first lane of group 0 for compile-time P: with pushed rotations (QEC_ROT_PUSH) the G = 64 / P
-// groups take the top G P lanes and the 64 - G P idle lanes sit below them, else the groups start at lane 0.
+// The first lane of group 0 for compile-time P: with pushed rotations the G = 64 / P groups take the top
+// G P lanes and the 64 - G P idle lanes sit below them, else the groups start at lane 0.
 template <int P_>
 constexpr int group_base()
 {
-    return (QEC_ROT_PUSH && 2 * P_ > 64 && P_ < 64) ? 64 - (64 / P_) * P_ : 0;
+    return (2 * P_ > 64 && P_ < 64) ? 64 - (64 / P_) * P_ : 0;
 }
 
-// Rotations by push (QEC_ROT_PUSH) for compile-time one-group waves.  The code also handles several
-// groups per wave (every shift pushed, groups on the top lanes), but for P7 it measured -1.8 .. +0.5 %
-// (profiles/r05/cmp_rot_push.txt), so multi-group waves keep their pulls.
+// Rotations by push for compile-time one-group waves (above).
 template <class SH>
 constexpr bool kPushRot()
 {
-    return QEC_ROT_PUSH && SH::kStatic && 2 * SH::kP > 64 && SH::kP < 64;
+    return SH::kStatic && 2 * SH::kP > 64 && SH::kP < 64;
 }
 template <class SH>
 constexpr int kGroupBase()
@@ -423,7 +199,7 @@ struct BpArgs {
     int hardPaths;  // QEC_HP_* bits: hard-message paths / cycle jump (QEC_OPT_HARD_PATHS, QEC_OPT_CYCLE_JUMP)
     int scaled;     // p' in [2^-20, 1/2] (scaled_ok): var passes with at most 4 factors per fold divide guard-free
     // lane-relabelled circulant tables (see relabel() below)
-    // iteration-0 tables of both sectors computed on the host (QEC_TABLE0_HOST: the same operations,
+    // iteration-0 tables of both sectors computed on the host (launch_decode: the same operations,
     // so the same bits, as table0_entry on the device; each workgroup copies them to LDS)
     float tab0[kMaxTab0];
     // zero-syndrome outcome of each sector under the fixed / reference stop (zero_outcome; 0: none):
@@ -525,33 +301,6 @@ struct GeneratedShifts {
     __device__ static constexpr int coloff(const BpArgs&, int l) { return SEC ? tabs.CZ[l] : tabs.CX[l]; }
 };
 
-// ---- experiment stamps (QEC_LIST_STAMPS) ------------------------------------
-#if QEC_LIST_STAMPS
-// [0..7] summed phase spans, [8..15] counts: added up per workgroup in LDS (one wave per workgroup:
-// lane 0's plain adds), flushed to g_list_stamps once per workgroup at the kernel's end
-static __device__ unsigned long long g_list_stamps[16];
-__device__ __forceinline__ unsigned long long* stamp_lds()
-{
-    __shared__ unsigned long long s[16];
-    return s;
-}
-__device__ __forceinline__ unsigned long long stamp_now()
-{
-    unsigned long long t;
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-    __builtin_amdgcn_sched_barrier(0);
-    return t;
-}
-__device__ __forceinline__ void stamp_add(int k, unsigned long long dt, unsigned long long n = 1)
-{
-    if (__lane_id() == 0) {
-        stamp_lds()[k] += dt;
-        stamp_lds()[8 + k] += n;
-    }
-}
-#endif
-
 // ---- lane helpers ----------------------------------------------------------
 __device__ __forceinline__ float bperm(int addr, float v)
 {
@@ -608,23 +357,13 @@ __device__ __forceinline__ int lane_i(const Lane& ln)
         return ln.i;
 }
 
-//   QEC_MASK_REMAT   one-group waves (P > 32): each rotation's lane mask is made at its use, s_bfm_b64 of the
-//                    shift, instead of a constant the compiler hoists out of the loops (where ~60 of them,
-//                    two SGPRs each, spill into VGPR lanes and come back with v_readlane)
-#ifndef QEC_MASK_REMAT
-#define QEC_MASK_REMAT 0
-#endif
+// (Rotation masks made at their use with s_bfm_b64 instead of hoisted constants, which spill into VGPR
+// lanes: -3.5 % on the headline, profiles/r05/cmp_mask_remat_headline.txt.)
 template <class SH>
 __device__ __forceinline__ int rot_addr(const Lane& ln, int s)
 {
     int base;
-    if constexpr (SH::kStatic && SH::kMaskSelect && QEC_MASK_REMAT && 2 * SH::kP > 64) {
-        int sv = s;
-        asm volatile("" : "+s"(sv));  // the shift is re-materialised here, so the mask is made here too
-        unsigned long long m;
-        asm("s_bfm_b64 %0, %1, %2" : "=s"(m) : "s"(sv), "s"(kGroupBase<SH>()));  // the group's lanes below s
-        base = select_lanes(ln.b0, ln.b1, m);
-    } else if constexpr (SH::kStatic && SH::kMaskSelect)
+    if constexpr (SH::kStatic && SH::kMaskSelect)
         base = select_lanes(ln.b0, ln.b1, lanes_below<SH::kP>(s));
     else
         base = (ln.i < s) ? ln.b1 : ln.b0;  // loop-invariant per s: hoisted by the compiler
@@ -635,7 +374,7 @@ template <class SH>
 __device__ __forceinline__ int rot_i(int v, const Lane& ln, int s)
 {
     if constexpr (kPushRot<SH>()) {
-        if (s != 0 && (2 * SH::kP < 64 || (QEC_ROT_PUSH_HI ? s >= SH::kP - 31 : s <= 31))) {
+        if (s != 0 && (2 * SH::kP < 64 || s >= SH::kP - 31)) {
             // the same rotation as a push: lane i's value goes to lane (i + s) mod P of its group.  The
             // address is (i < P - s ? b1 : b0) + (256 + 4 s - 4 P): lane gb + i + s or gb + i + s - P, mod 64
             int base;
@@ -736,31 +475,6 @@ __device__ __forceinline__ bool div_short_ok(float n, float d)
 // the IEEE division in those passes).
 __host__ __device__ inline bool scaled_ok(float pp) { return pp >= 0x1p-20f && pp <= 0.5f; }
 
-//   QEC_PATH_STATS   experiment builds only: count, per sector, the var-pass columns taking each
-//                    path (same / zero / short division / full division; soft or hard inputs)
-#ifndef QEC_PATH_STATS
-#define QEC_PATH_STATS 0
-#endif
-#ifndef QEC_EXP_SHORTALL
-#define QEC_EXP_SHORTALL 0
-#endif
-#if QEC_PATH_STATS
-static __device__ unsigned long long g_path_stats[24];
-#if defined(QEC_P61_MINREG_TU)
-}  // namespace qec
-extern "C" int qec_debug_path_stats(unsigned long long* out, int reset)
-{
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(qec::g_path_stats), sizeof(qec::g_path_stats)) != hipSuccess) return -1;
-    if (reset) {
-        static const unsigned long long z[24] = {};
-        if (hipMemcpyToSymbol(HIP_SYMBOL(qec::g_path_stats), z, sizeof z) != hipSuccess) return -1;
-    }
-    return 0;
-}
-namespace qec {
-#endif
-#endif
-
 // ---- one sector (X: R = J, Z: R = K) ------------------------------------
 // EqNodeUpdate (DecoderCPU.h:150-186) for checks (r, i), r = 0..R-1: lane-local.
 template <int R, int L, bool RB = false>
@@ -829,30 +543,6 @@ __device__ __forceinline__ bool zero_ok(float pp)
     return F <= 5 && pp >= 0.0f && pp <= 0.5f;
 }
 
-// true iff every division of the coming var pass lies in the short form's domain, on every live
-// lane (zero_ok required): each numerator is a left fold p' * g_a * g_b * ... over F incoming
-// check messages g in [0, 1] (or NaN); if one of them is 0 so is the numerator, and otherwise, as
-// rounding is monotone, the numerator is at least the same fold with every factor replaced by the
-// smallest nonzero incoming message m; when that bound is >= 2^-98 so is every nonzero numerator.
-// A NaN message never lowers m and yields NaN through the short form, as through the IEEE
-// division.  The wave-wide test does not depend on the lane layout, so it runs on the check view.
-template <int R, int L, bool LAST, class SH>
-__device__ __forceinline__ bool short_domain(const float (&msg)[R][L], float pp, bool live)
-{
-    uint32_t m = 0xFFFFFFFFu;  // smallest nonzero message bits, minus one (+0 wraps to the top)
-#pragma unroll
-    for (int r = 0; r < R; ++r)
-#pragma unroll
-        for (int l = 0; l < L; ++l) m = min(m, __float_as_uint(msg[r][l]) - 1u);
-    const float mf = m == 0xFFFFFFFFu ? 1.0f : __uint_as_float(m + 1u);
-    float b = pp;
-#pragma unroll
-    for (int k = 0; k < (LAST ? R : R - 1); ++k) b = b * mf;
-    // the uniform zero_ok is AND-ed to the ballot's scalar result, not into the per-lane predicate (that
-    // materialised the predicate as an integer and back, two VALU per ballot)
-    return band(all_live_sh<SH>(__float_as_uint(b) >= __float_as_uint(0x1p-98f), live), zero_ok<R, LAST>(pp));
-}
-
 // Syndrome stop with one group per wave (compile-time P > 32): the var pass stores its outgoing messages
 // in the variable view (msg[r][l] = variable (l, .)'s message on edge r) instead of rotating each back to
 // its check at once.  The stop test needs only the decisions, and the post-processing of a stopped
@@ -862,7 +552,7 @@ __device__ __forceinline__ bool short_domain(const float (&msg)[R][L], float pp,
 template <bool HD, class SH>
 constexpr bool defer_return()
 {
-    if constexpr (SH::kStatic) return HD && QEC_SYN_DEFER_RETURN && 2 * SH::kP > 64;
+    if constexpr (SH::kStatic) return HD && 2 * SH::kP > 64;
     else return false;
 }
 
@@ -895,32 +585,25 @@ __device__ __forceinline__ void return_pass(const BpArgs& a, float (&msg)[R][L],
 // compiler schedules CG columns' products, divisions and rotations as one straight-line block.
 // CG > 1 requires soft inputs (hard == false on entry): the hard-input agreement shortcut below
 // works column by column.
-// ALLFAST: the caller proved every division of this pass inside the short form's domain
-// (short_domain below), so no column evaluates the guard: the pass is straight-line code.
-template <int R, int L, int SEC, bool LAST, bool HD, class SH, class TU, int CG = 1, bool ALLFAST = false,
-          bool SOFT_IN = false>
+// SOFT_IN: the caller knows the inputs are soft, so no column takes the agreeing-inputs branch (soft
+// passes are straight-line code per column group: P61 headline +3.6 %, P7 +1 %;
+// profiles/r03/cmp_soft_straight_*.txt).
+template <int R, int L, int SEC, bool LAST, bool HD, class SH, class TU, int CG = 1, bool SOFT_IN = false>
 __device__ __forceinline__ uint32_t var_pass(const BpArgs& a, float (&msg)[R][L], const Lane& ln, float pp,
-                                             float one_minus_pp, bool& hard, bool& vagree, bool track = true,
-                                             bool* ident = nullptr)
+                                             float one_minus_pp, bool& hard, bool& vagree, bool track = true)
 {
     static_assert(L % CG == 0, "column groups must tile the L columns");
-    const bool hard_in = !SOFT_IN && CG == 1 && hard;  // SOFT_IN: the caller knows the inputs are soft
-    // ident (out, hard inputs): every column took the agreeing-inputs shortcut below, i.e. the pass was the
-    // identity on the check-view registers -- the agreement path, found without var_pass_agree's gathers
-    bool all_done = hard_in;
+    const bool hard_in = !SOFT_IN && CG == 1 && hard;
     bool vsame = true;  // this lane's variables: all R outputs equal (float compare: NaN is unequal)
     uint32_t soft_bits = 0;  // OR of bits(q - q*q) over the outputs: 0 iff all are 0 or 1
-    // the short division's guard assumes every message is a probability in [0, 1], which
-    // holds by induction when p' is (DecoderCPU.h:135-229); other p' always take the full path
-    const bool pp_ok = pp >= 0.0f && pp <= 1.0f;
     constexpr int F = LAST ? R : R - 1;  // factors per fold
-    constexpr bool kScalable = TU::kFastDiv && F <= 4 && QEC_SCALED_DIV;
-    const bool scaled = kScalable && (QEC_ASSUME_SCALED || a.scaled);  // wave-uniform (see scaled_ok)
+    constexpr bool kScalable = TU::kFastDiv && F <= 4;
+    const bool scaled = kScalable && a.scaled;  // wave-uniform (see scaled_ok)
     const float fold0 = scaled ? one_minus_pp * 0x1p32f : one_minus_pp, fold1 = scaled ? pp * 0x1p32f : pp;
     const int P = SH::P(a);
     const int* et = SH::template table<SEC>(a);
     uint32_t hdmask = 0;
-    // QEC_PIPELINE = D: the gathers of columns l + 1 .. l + D are in flight while column l is
+    // TU::kPipeline = D: the gathers of columns l + 1 .. l + D are in flight while column l is
     // computed, so their ds_bpermute latency hides behind column l's arithmetic in the same wave
     // (the per-group uniform branches below end basic blocks, so the compiler cannot do this).
     constexpr int D = TU::kPipeline > 0 ? (TU::kPipeline < L ? TU::kPipeline : L - 1) : 0;
@@ -969,13 +652,9 @@ __device__ __forceinline__ uint32_t var_pass(const BpArgs& a, float (&msg)[R][L]
 #pragma unroll
                     for (int r = 0; r < R; ++r) qv[0][r] = gv[0][0];
                     done = true;
-#if QEC_PATH_STATS
-                    if (__lane_id() == 0) atomicAdd(&g_path_stats[SEC * 8 + 4], 1ull);
-#endif
                 }
             }
         }
-        all_done = band(all_done, done);
         if (!done) {
             // numerators / denominators of the outgoing messages, left folds in ascending k
             float num[CG][ND], den[CG][ND];
@@ -1005,7 +684,7 @@ __device__ __forceinline__ uint32_t var_pass(const BpArgs& a, float (&msg)[R][L]
             }
             float qd[CG][ND];
             bool zero = false, fast = false;
-            if constexpr (TU::kZeroSkip && !ALLFAST) {
+            if constexpr (TU::kZeroSkip) {
                 uint32_t nb = 0;
                 bool dpos = true;
 #pragma unroll
@@ -1017,66 +696,20 @@ __device__ __forceinline__ uint32_t var_pass(const BpArgs& a, float (&msg)[R][L]
                     }
                 zero = all_live(nb == 0u && dpos, ln.live);
             }
-            if constexpr (ALLFAST) {
-                fast = true;
-            } else if constexpr (kScalable) {
+            if constexpr (kScalable) {
                 fast = scaled;  // no guard (scaled folds); other p' take the IEEE division
             } else if constexpr (TU::kFastDiv) {
-                if constexpr (QEC_GUARD_ZERO != 0) {
-                    // numerators outside (0, 2^-98): minima of their bit patterns minus one, +0
-                    // wrapping to the top.  Needs zero_ok (p' <= 1/2, a wave-uniform AND, no
-                    // branch); other p' (p > 3/4, never a decoding regime) always take the IEEE
-                    // division.
-                    uint32_t nm = 0xFFFFFFFFu;
-#pragma unroll
-                    for (int c = 0; c < CG; ++c)
-#pragma unroll
-                        for (int j = 0; j < ND; ++j) nm = min(nm, __float_as_uint(num[c][j]) - 1u);
-                    fast = band(all_live_sh<SH>(nm >= __float_as_uint(0x1p-98f) - 1u, ln.live), zero_ok<R, LAST>(pp));
-                } else if (!zero) {
-                    // the guard of every division of the group at once, as unsigned minima of bit
-                    // patterns (non-negative floats order like their bits): numerators minus 1 (+0
-                    // wraps to the top), denominators as they are.  A NaN sorts above every
-                    // number, so it never fails the guard; the short form then returns NaN, as the
-                    // IEEE division does.
-                    uint32_t nm = 0xFFFFFFFFu, dm = 0xFFFFFFFFu;
-#pragma unroll
-                    for (int c = 0; c < CG; ++c)
-#pragma unroll
-                        for (int j = 0; j < ND; ++j) {
-                            nm = min(nm, __float_as_uint(num[c][j]) - 1u);
-                            dm = min(dm, __float_as_uint(den[c][j]));
-                        }
-                    const bool ok = (int)(dm >= __float_as_uint(0x1p-98f)) & (int)(nm >= __float_as_uint(0x1p-98f) - 1u);
-                    fast = pp_ok && all_live_sh<SH>(ok, ln.live);
-                }
-            }
-#if QEC_EXP_SHORTALL
-            fast = pp_ok && !zero;  // timing experiment only: the guard ignored (outputs may differ)
-#endif
-#if QEC_PATH_STATS
-            if (__lane_id() == 0)
-                atomicAdd(&g_path_stats[SEC * 8 + (hard_in ? 4 : 0) + (zero ? 1 : fast ? 2 : 3)], (unsigned long long)CG);
-            {
-                // guard anatomy of the group: every n >= 2^-98 / zeros but no tiny nonzero n and every
-                // d >= 2^-98 / a tiny nonzero n / some d < 2^-98
-                bool anyz = false, tiny = false, dsmall = false, allbig = true;
+                // numerators outside (0, 2^-98): minima of their bit patterns minus one, +0 wrapping to
+                // the top.  The guard assumes every message is a probability in [0, 1] (true by induction
+                // for such p', DecoderCPU.h:135-229) and needs zero_ok (p' <= 1/2, a wave-uniform AND, no
+                // branch); other p' (p > 3/4, never a decoding regime) always take the IEEE division.
+                uint32_t nm = 0xFFFFFFFFu;
 #pragma unroll
                 for (int c = 0; c < CG; ++c)
 #pragma unroll
-                    for (int j = 0; j < ND; ++j) {
-                        const uint32_t nb = __float_as_uint(num[c][j]);
-                        anyz |= nb == 0u;
-                        tiny |= nb != 0u && nb < __float_as_uint(0x1p-98f);
-                        dsmall |= __float_as_uint(den[c][j]) < __float_as_uint(0x1p-98f);
-                        allbig &= nb >= __float_as_uint(0x1p-98f);
-                    }
-                const bool wz = __ballot(anyz && ln.live) != 0ull, wt = __ballot(tiny && ln.live) != 0ull;
-                const bool wd = __ballot(dsmall && ln.live) != 0ull, wb = __ballot(!allbig && ln.live) == 0ull;
-                const int k = wb ? 0 : wt ? 2 : wd ? 3 : wz ? 1 : 3;
-                if (__lane_id() == 0 && !hard_in) atomicAdd(&g_path_stats[16 + SEC * 4 + k], (unsigned long long)CG);
+                    for (int j = 0; j < ND; ++j) nm = min(nm, __float_as_uint(num[c][j]) - 1u);
+                fast = band(all_live_sh<SH>(nm >= __float_as_uint(0x1p-98f) - 1u, ln.live), zero_ok<R, LAST>(pp));
             }
-#endif
             if (zero) {
 #pragma unroll
                 for (int c = 0; c < CG; ++c)
@@ -1125,14 +758,15 @@ __device__ __forceinline__ uint32_t var_pass(const BpArgs& a, float (&msg)[R][L]
                 msg[r][l] = defer_return<HD, SH>() ? qv[c][r] : rot<SH>(qv[c][r], ln, sh == 0 ? 0 : P - sh);
             }
         }
-        if constexpr (QEC_COL_BARRIER) __builtin_amdgcn_sched_barrier(0);  // see QEC_COL_BARRIER
+        // a scheduling barrier after each column group: the machine scheduler otherwise hoists work
+        // across columns into more live registers (P61 headline +2.8 %, profiles/r03/cmp_col_barrier_*.txt)
+        __builtin_amdgcn_sched_barrier(0);
     }
     if constexpr (TU::kSaturate) {
         const bool forms = track && (a.hardPaths & QEC_HP_FORMS) && hard_ok(pp);
         hard = forms && all_live_sh<SH>(soft_bits == 0u, ln.live);
         vagree = hard && all_live_sh<SH>(vsame, ln.live);
     }
-    if (ident != nullptr) *ident = all_done;
     return hdmask;
 }
 
@@ -1190,62 +824,19 @@ __device__ __forceinline__ bool lane_syndrome_ok(const BpArgs& a, uint32_t hdmas
             x ^= ((uint32_t)rot_i<SH>((int)hdmask, ln, sh == 0 ? 0 : P - sh) >> l) & 1u;
         }
         match &= (x == ((sbits >> r) & 1u));
-#if QEC_SYN_ROWBARRIER
         // one row's L rotations in flight at a time: all R L at once (the scheduler's choice) held
         // R L results live beside the sector's messages and spilled the syndrome-stop kernels
         __builtin_amdgcn_sched_barrier(0);
-#endif
     }
     return match && !(sbits & kNonBinary);
 }
 
-// The same test for a whole group, from ballots instead of rotations (compile-time shifts): bit mu of
-// H_l = ballot(hard decision of column l) is variable (l, (mu + C[l]) mod P) of its group, so the
-// decision's syndrome on check-view lane lambda of row r is XOR_l H_l[(lambda + S[r][l]) mod P] -- a
-// cyclic rotation of each group's P bits of H_l by S[r][l], done in scalar registers.  The wave's
-// mismatches (input syndrome ballot XOR that, or a non-binary entry) then decide each group at once: no
-// ds_bpermute (R L of them in lane_syndrome_ok) and no VGPR temporaries.  Ballots see the lanes running
-// the call, i.e. the active groups; rotations stay inside a group, so other groups' bits never mix in.
-template <int P>
-__host__ __device__ constexpr unsigned long long group_bits_below(int s)  // bit g P + i for i < s, every group
-{
-    unsigned long long m = 0;
-    for (int g = 0; g < 64 / P; ++g)
-        for (int i = 0; i < s; ++i) m |= 1ull << (g * P + i);
-    return m;
-}
-template <int P>
-__device__ __forceinline__ unsigned long long rotr_groups(unsigned long long x, int s)  // bit gP+i <- bit gP+(i+s)%P
-{
-    if (s == 0) return x;
-    if constexpr (2 * P > 64) return (x >> s) | (x << (P - s));  // one group: bits >= P are cleared by the caller
-    else return ((x >> s) & group_bits_below<P>(P - s)) | ((x << (P - s)) & ~group_bits_below<P>(P - s));
-}
+// The same test for a whole group.  (From ballots and scalar rotations instead of ds_bpermute: 5-8 %
+// slower, SALU-bound; profiles/r05/README.md.)
 template <int R, int L, int SEC, class SH>
 __device__ __forceinline__ bool group_syndrome_ok(const BpArgs& a, uint32_t hdmask, uint32_t sbits, const Lane& ln)
 {
-    if constexpr (SH::kStatic && QEC_SYN_BALLOT) {
-        constexpr int P = SH::kP;
-        unsigned long long H[L];
-#pragma unroll
-        for (int l = 0; l < L; ++l) H[l] = __ballot((hdmask >> l) & 1u);
-        unsigned long long bad = __ballot((sbits & kNonBinary) != 0u);
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            unsigned long long syn = __ballot((sbits >> r) & 1u);
-#pragma unroll
-            for (int l = 0; l < L; ++l) syn ^= rotr_groups<P>(H[l], SH::template shift<SEC, L>(nullptr, r, l));
-            bad |= syn;
-        }
-        bad &= group_bits_below<P>(P);
-        if constexpr (2 * P > 64) {
-            return bad == 0ull;
-        } else {
-            return ((bad >> ln.gb) & ((1ull << P) - 1ull)) == 0ull;
-        }
-    } else {
-        return group_all_sh<SH>(lane_syndrome_ok<R, L, SEC, SH>(a, hdmask, sbits, ln), ln, SH::P(a));
-    }
+    return group_all_sh<SH>(lane_syndrome_ok<R, L, SEC, SH>(a, hdmask, sbits, ln), ln, SH::P(a));
 }
 
 // Whether a hard sector first tries the whole-sector agreement test (var_pass_agree, the entry to
@@ -1259,7 +850,7 @@ __device__ __forceinline__ bool group_syndrome_ok(const BpArgs& a, uint32_t hdma
 template <int STOP, class TU>
 constexpr bool kAgree()
 {
-    return QEC_AGREE && (STOP != QEC_STOP_SYNDROME || QEC_AGREE_SYN || TU::kAgreeSyn);
+    return STOP != QEC_STOP_SYNDROME || TU::kAgreeSyn;
 }
 
 // Row 0 of the syndrome test is lane-local when every block of row 0 has rotation 0 (the relabelled
@@ -1267,7 +858,7 @@ constexpr bool kAgree()
 template <int SEC, int L, class SH>
 constexpr bool kRow0Local()
 {
-    if constexpr (!SH::kStatic || !QEC_SYN_ROW0_FIRST) {
+    if constexpr (!SH::kStatic) {
         return false;
     } else {
         for (int l = 0; l < L; ++l)
@@ -1276,9 +867,10 @@ constexpr bool kRow0Local()
     }
 }
 
-// QEC_SYN_SKIP_SEEN for L columns (the never-seen marker ~0u is no decision mask when L < 32)
+// The syndrome stop's repeated-decision skip (iteration) for L columns (the never-seen marker ~0u is no
+// decision mask when L < 32)
 template <int L>
-constexpr bool kSkipSeen() { return QEC_SYN_SKIP_SEEN && L < 32; }
+constexpr bool kSkipSeen() { return L < 32; }
 
 // One BP iteration; returns true if this group stops after it.
 // hard: every variable->check message of this sector is exactly +0 or 1.0 (wave-uniform).
@@ -1307,32 +899,21 @@ __device__ __forceinline__ bool iteration(const BpArgs& a, float (&msg)[R][L], u
             vagree = true;
             var_layout = false;  // the agreement path leaves the check-view registers as they are
         } else {
-            // without the agreement test (syndrome stop): a pass whose every column took the agreeing-inputs
-            // shortcut was the agreement path all the same (var_pass's ident), which the cycle jump needs
-            bool ident = false;
-            hdmask = var_pass<R, L, SEC, LAST, HD, SH, TU>(a, msg, ln, pp, one_minus_pp, hard, vagree, true,
-                                                           QEC_IDENT_AGREE ? &ident : nullptr);
-            agreed = ident;
+            // (without the agreement test, a pass whose every column took the agreeing-inputs shortcut could
+            // count as the agreement path: 0-6 % slower, profiles/r05/README.md)
+            hdmask = var_pass<R, L, SEC, LAST, HD, SH, TU>(a, msg, ln, pp, one_minus_pp, hard, vagree, true);
         }
     } else {
         check_pass<R, L, TU::kRowBarrier>(msg, sbits);
-        // the hard-state test is skipped in the first QEC_TRACK_FROM iterations (they essentially
-        // never end hard; skipping only delays the exact hard forms, never changes a bit)
-        // hard == false here, so the soft inputs allow column groups (var_pass)
+        // the hard-state test is skipped in the first kTrackFrom iterations (they essentially never end
+        // hard; skipping only delays the exact hard forms, never changes a bit), and not at all when the
+        // hard-message forms are off (QEC_OPT_HARD_PATHS = 0): the test only feeds them (var_pass returns
+        // hard = false either way).  hard == false here, so the soft inputs allow column groups and a
+        // straight-line pass (var_pass's CG, SOFT_IN).  (One division branch per pass instead of per column
+        // group: P61 2x slower, profiles/r03/cmp_soft_straight_*.txt.)
         constexpr int CG = col_group<TU, L>();
-        // and not at all when the hard-message forms are off (QEC_OPT_HARD_PATHS = 0): the test only
-        // feeds them (var_pass returns hard = false either way)
-        const bool track = (LAST || n >= QEC_TRACK_FROM) && (a.hardPaths & QEC_HP_FORMS);
-        // soft inputs (SOFT_IN): no per-column agreement branch; with the scaled short division in this
-        // pass (QEC_SOFT_STRAIGHT = 2) no per-column division branch either -- one branch for the pass
-        constexpr bool kStraight = QEC_SOFT_STRAIGHT >= 1;
-        constexpr bool kScal = TU::kFastDiv && (LAST ? R : R - 1) <= 4 && QEC_SCALED_DIV;
-        if (QEC_SOFT_STRAIGHT >= 2 && kScal && a.scaled)
-            hdmask = var_pass<R, L, SEC, LAST, HD, SH, TU, CG, true, true>(a, msg, ln, pp, one_minus_pp, hard, vagree, track);
-        else if (QEC_GUARD_GLOBAL && TU::kFastDiv && zero_ok<R, LAST>(pp) && short_domain<R, L, LAST, SH>(msg, pp, ln.live))
-            hdmask = var_pass<R, L, SEC, LAST, HD, SH, TU, CG, true, kStraight>(a, msg, ln, pp, one_minus_pp, hard, vagree, track);
-        else
-            hdmask = var_pass<R, L, SEC, LAST, HD, SH, TU, CG, false, kStraight>(a, msg, ln, pp, one_minus_pp, hard, vagree, track);
+        const bool track = (LAST || n >= kTrackFrom) && (a.hardPaths & QEC_HP_FORMS);
+        hdmask = var_pass<R, L, SEC, LAST, HD, SH, TU, CG, true>(a, msg, ln, pp, one_minus_pp, hard, vagree, track);
     }
     if constexpr (STOP == QEC_STOP_REF) {
         if (n % 10 == 0) return group_all_sh<SH>(lane_converged<R, L>(msg), ln, P);  // DecoderCPU.h:287-290
@@ -1359,7 +940,7 @@ __device__ __forceinline__ bool iteration(const BpArgs& a, float (&msg)[R][L], u
         if (!skip && !row0_fails) {
             // launder the bases again: the test's rotations are var_pass's return rotations, whose
             // addresses would otherwise be kept live across the whole var pass for reuse here
-            if constexpr (SH::kMaskSelect && QEC_SYN_RELAUNDER) asm volatile("" : "+v"(ln.b0), "+v"(ln.b1));
+            if constexpr (SH::kMaskSelect) asm volatile("" : "+v"(ln.b0), "+v"(ln.b1));
             stop = group_syndrome_ok<R, L, SEC, SH>(a, hdmask, sbits, ln);
         }
         if (kSkipSeen<L>() && !same0) {
@@ -1439,7 +1020,7 @@ __device__ __forceinline__ bool iteration0(const BpArgs& a, float (&msg)[R][L], 
     const int* et = SH::template table<SEC>(a);
     constexpr bool HD = STOP == QEC_STOP_SYNDROME && !GO;
     msg_out = true;
-    if constexpr (HD && QEC_SYN_EARLY && L * R <= 64) {
+    if constexpr (HD && L * R <= 64) {
         // Syndrome stop: a variable's hard decision after this iteration, and whether its R
         // messages lie outside (0.01, 0.99), depend only on its syndrome pattern idx, so they come
         // from two 2^R-bit masks before any message is formed; the messages themselves (table
@@ -1521,7 +1102,7 @@ constexpr uint32_t kZsValid = 1u << 31;
 template <int R, int L>
 uint32_t zero_outcome(float pp, int N, int stop)
 {
-    if (!(pp > 0.0f && pp < 1.0f) || N < 2 || N > 0xFFFF || stop == QEC_STOP_SYNDROME || QEC_PHASE_STATS || !QEC_TABLE0)
+    if (!(pp > 0.0f && pp < 1.0f) || N < 2 || N > 0xFFFF || stop == QEC_STOP_SYNDROME || QEC_PHASE_STATS)
         return 0u;
     float q = table0_entry<R, L>(pp, 0);  // iteration 0 (syndrome pattern 0), as iteration0
     int it = 1;
@@ -1674,7 +1255,7 @@ __device__ __forceinline__ void decode_sector(const BpArgs& a, Lane& ln, uint32_
     // hard decision is 0 when every tab0[r] < 0.5, its syndrome is the input's (0), and the sector
     // stops after that iteration with e = 0, conv = every tab0[r] outside (0.01, 0.99).  The same
     // outputs without the iteration's rotations (not when the final messages are requested).
-    if constexpr (STOP == QEC_STOP_SYNDROME && QEC_TABLE0 && QEC_ZERO_SYNDROME && !GO) {
+    if constexpr (STOP == QEC_STOP_SYNDROME && !GO) {
         if (a.maxIter >= 2 && a.q == nullptr && all_live(sbits == 0u, in_range)) {
             bool low = true, cv = true;
 #pragma unroll
@@ -1691,9 +1272,6 @@ __device__ __forceinline__ void decode_sector(const BpArgs& a, Lane& ln, uint32_
         }
     }
 
-#if QEC_LIST_STAMPS
-    const unsigned long long ts0 = stamp_now();
-#endif
     // Zero syndrome under the fixed / reference stop: the launch's precomputed outcome (zero_outcome)
     if constexpr (STOP != QEC_STOP_SYNDROME) {
         const uint32_t zs = a.zs[SEC];
@@ -1731,13 +1309,13 @@ __device__ __forceinline__ void decode_sector(const BpArgs& a, Lane& ln, uint32_
     // syndrome test the same test, so they are reused (group-uniform).
     uint32_t hd_last = 0;
     bool syn_last = false, hd_valid = false;
-    uint32_t seen[2] = {~0u, ~0u};  // the group's last two tested (failed) hard decisions (QEC_SYN_SKIP_SEEN)
+    uint32_t seen[2] = {~0u, ~0u};  // the group's last two tested (failed) hard decisions (iteration's skip)
     // iteration 0 of the syndrome stop may leave the messages unformed (every group stopped there):
     // then cv0 is each lane's convergence test of them (iteration0)
     bool cv0 = true, msg_built = true;
     unsigned long long hdpat = 0, cvpat = 0;
-    if constexpr (STOP == QEC_STOP_SYNDROME && QEC_SYN_EARLY && QEC_TABLE0 && !GO) pattern_masks<R>(tab0, hdpat, cvpat);
-    if (QEC_TABLE0 && N >= 2 && active) {  // iteration 0 by table (see iteration0)
+    if constexpr (STOP == QEC_STOP_SYNDROME && !GO) pattern_masks<R>(tab0, hdpat, cvpat);
+    if (N >= 2 && active) {  // iteration 0 by table (see iteration0)
         ++it;
         syn_last = iteration0<R, L, SEC, STOP, SH, GO>(a, msg, sbits, ln, tab0, hd_last, cv0, msg_built, hdpat, cvpat);
         hd_valid = true;
@@ -1746,15 +1324,9 @@ __device__ __forceinline__ void decode_sector(const BpArgs& a, Lane& ln, uint32_
         if constexpr (QEC_PHASE_STATS) ph_soft += 1;
         n = 1;
     }
-#if QEC_LIST_STAMPS
-    const unsigned long long ts1 = stamp_now();
-#endif
     // iterations n .. N-2 (DecoderCPU.h:280-291); the last one is peeled below
     for (; n < N - 1; ++n) {
         if (!__any(active)) break;  // DecoderCPU.h:282 (fixed: only after a cycle jump)
-        if constexpr (QEC_LONG_PRIO > 0) {
-            if (n == QEC_LONG_PRIO) __builtin_amdgcn_s_setprio(3);
-        }
         if (active) {
             ++it;
             const bool was_hard = hard;
@@ -1790,13 +1362,6 @@ __device__ __forceinline__ void decode_sector(const BpArgs& a, Lane& ln, uint32_
         st_agreed = vagree;
     }
 
-    if constexpr (QEC_ABLATE == 1) {
-        iters_out = it + (int)__float_as_uint(msg[0][0]);
-        return;
-    }
-#if QEC_LIST_STAMPS
-    const unsigned long long ts2 = stamp_now();
-#endif
     // ---- post-processing of Decode (DecoderCPU.h:354-384) ----
     asm volatile("" : "+v"(sbits));  // its per-row bits are recomputed here, not held since the sector began
     const int* et = SH::template table<SEC>(a);
@@ -1841,19 +1406,7 @@ __device__ __forceinline__ void decode_sector(const BpArgs& a, Lane& ln, uint32_
         }
         syn_ok = group_syndrome_ok<R, L, SEC, SH>(a, hdmask, sbits, ln);
     }
-#if QEC_LIST_STAMPS
-    const unsigned long long ts3 = stamp_now();
-#endif
     emit_decisions<L, SEC, SH>(a, ln, b, in_range, hdmask, stage);
-#if QEC_LIST_STAMPS
-    const unsigned long long ts4 = stamp_now();
-    if (STOP == QEC_STOP_SYNDROME) {
-        stamp_add(4 * SEC + 0, ts1 - ts0);
-        stamp_add(4 * SEC + 1, ts2 - ts1, (unsigned long long)(it > 1 ? it - 1 : 0));
-        stamp_add(4 * SEC + 2, ts3 - ts2);
-        stamp_add(4 * SEC + 3, ts4 - ts3);
-    }
-#endif
 
     if (!syn_ok) flags |= SEC ? QEC_SYNDROME_FAIL_Z : QEC_SYNDROME_FAIL_X;
     if (!conv) flags |= SEC ? QEC_CONVERGENCE_FAIL_Z : QEC_CONVERGENCE_FAIL_X;
@@ -1874,37 +1427,23 @@ __device__ __forceinline__ void decode_sector(const BpArgs& a, Lane& ln, uint32_
 // satisfied its syndrome already (P61 at p = 0.02 .. 0.1: no hard iteration among 16 384 syndromes,
 // tools/kbench/phase_hist.py, profiles/r06/phase_hist.txt), so tracking the hard state -- an fma and an
 // OR per outgoing message and a compare per column in every soft var pass, ~10 % of a P61 soft iteration
-// -- and the hard branches' registers are pure cost there.
-//   QEC_SYN_HARD  1: the syndrome-stop kernels keep the hard-message forms (the round-5 kernels)
-#ifndef QEC_SYN_HARD
-#define QEC_SYN_HARD 0
-#endif
+// -- and the hard branches' registers are pure cost there: config 5 +2 % (p = 2e-3) .. +10 % (p = 0.1),
+// profiles/r06/ab/cmp_syn_soft_vs_hard.txt.
 template <class TU>
 struct SoftTune : TU {
     static constexpr bool kSaturate = false;
 };
 // Taken for one-group waves (P61); P7's syndrome-stop kernels (nine groups per wave) keep the forms.
 template <int STOP, class SH, class TU>
-using StopTune = typename std::conditional<STOP == QEC_STOP_SYNDROME && !QEC_SYN_HARD && SH::kStatic && (2 * SH::kP > 64),
+using StopTune = typename std::conditional<STOP == QEC_STOP_SYNDROME && SH::kStatic && (2 * SH::kP > 64),
                                            SoftTune<TU>, TU>::type;
-
-// Tuning knobs (compile-time; tools/kbench/ sweeps them).
-#ifndef QEC_WAVES_PER_BLOCK
-#define QEC_WAVES_PER_BLOCK 0   // 0: per-variant (Tune<>::kWavesPerBlock)
-#endif
-#ifndef QEC_MIN_WAVES_PER_EU
-#define QEC_MIN_WAVES_PER_EU 0  // 0: per-variant defaults below
-#endif
-#ifndef QEC_SYN_MINW_DELTA
-#define QEC_SYN_MINW_DELTA 0    // experiment: the syndrome-stop kernels' min waves per SIMD, relative
-#endif
 
 // MINW: minimum waves per SIMD the register allocator must allow (5 -> <= 96 VGPRs), measured
 // per variant with tools/kbench (P61: 5 waves beat 4 by 4 %; see profiles/).
 // SPLIT: waves 2k and 2k+1 decode sectors X and Z of group k (adjacent waves; they meet in a global merge word);
 // the launch zeroed flags[] and each sector ORs in its bits.  Otherwise one wave decodes both.
 template <class TU>
-constexpr int waves_per_block() { return QEC_WAVES_PER_BLOCK > 0 ? QEC_WAVES_PER_BLOCK : TU::kWavesPerBlock; }
+constexpr int waves_per_block() { return TU::kWavesPerBlock; }
 
 // The syndrome pair b (or, with one sector per wave, its sector doX ? X : Z) of this lane's group:
 // decode, then the flags byte and iteration counts.  MODE (see bp_decode_kernel) 0: both sectors,
@@ -1913,14 +1452,12 @@ constexpr int waves_per_block() { return QEC_WAVES_PER_BLOCK > 0 ? QEC_WAVES_PER
 // (stores its flags in the syndrome's merge word), 4: sector Z of a sector launch, enqueued after the X
 // launch on the same stream (stores the flags byte: the merge word OR its own flags).  Modes 3 and 4
 // compile one sector only, so each kernel's registers are allocated for that sector alone.
-// pre: the sector's syndrome bits were loaded by the caller (sbPre; list mode, one sector per wave)
 template <int RX, int RZ, int L, int STOP, class SH, class TU, int MODE>
 __device__ __forceinline__ void decode_group(const BpArgs& a, const float* __restrict__ tab0, uint8_t* __restrict__ stage,
-                                             int i, int gb, uint32_t b, bool in_range, bool doX, bool pre = false,
-                                             uint32_t sbPre = 0u)
+                                             int i, int gb, uint32_t b, bool in_range, bool doX)
 {
     constexpr bool SPLIT = MODE != 0;
-    constexpr bool kHasX = MODE != 4 && MODE != 6, kHasZ = MODE != 3 && MODE != 5;
+    constexpr bool kHasX = MODE != 4, kHasZ = MODE != 3;
     constexpr int kTabX = (1 << RX) * RX;
     // p' = (2/3) p, as the reference writes it (DecoderCPU.h:259)
     const float pp = 2.0f / 3.0f * a.errorProbability;
@@ -1928,20 +1465,16 @@ __device__ __forceinline__ void decode_group(const BpArgs& a, const float* __res
     uint32_t flags = 0;
     int itX = 0, itZ = 0;
     Lane ln{i, gb, 4 * (gb + i), 4 * (gb + i + P), in_range};
-#ifndef QEC_PREFETCH_Z
-#define QEC_PREFETCH_Z 1
-#endif
     const bool runX = kHasX && doX, runZ = kHasZ && (!doX || !SPLIT);
     // list mode: every listed sector goes on past iteration 0 (decode_sector's GO)
-    constexpr bool GO = QEC_LIST_GO && (MODE == 2 || MODE == 5 || MODE == 6);
+    constexpr bool GO = MODE == 2;
     // both sectors' syndrome loads are issued up front: the Z load's latency hides behind X
-    const uint32_t sbX = pre ? sbPre : runX ? load_sbits<RX, 0, SH>(a, ln, b, in_range) : 0u;
-    uint32_t sbZ = pre ? sbPre : (QEC_PREFETCH_Z && runZ) ? load_sbits<RZ, 1, SH>(a, ln, b, in_range) : 0u;
+    const uint32_t sbX = runX ? load_sbits<RX, 0, SH>(a, ln, b, in_range) : 0u;
+    const uint32_t sbZ = runZ ? load_sbits<RZ, 1, SH>(a, ln, b, in_range) : 0u;
     if constexpr (kHasX) {
         if (runX) decode_sector<RX, L, 0, STOP, SH, TU, GO>(a, ln, b, in_range, pp, sbX, tab0, flags, itX, stage);
     }
     if constexpr (kHasZ) {
-        if (!pre && !QEC_PREFETCH_Z && runZ) sbZ = load_sbits<RZ, 1, SH>(a, ln, b, in_range);
         if (runZ) decode_sector<RZ, L, 1, STOP, SH, TU, GO>(a, ln, b, in_range, pp, sbZ, tab0 + kTabX, flags, itZ, stage);
     }
     if (in_range && lane_i<SH>(ln) == 0) {
@@ -1952,7 +1485,7 @@ __device__ __forceinline__ void decode_group(const BpArgs& a, const float* __res
             a.merge[b] = flags;  // for the Z launch (a word per syndrome, not the record's byte: one line each)
         } else if constexpr (MODE == 4) {
             *fdst = (uint8_t)(a.merge[b] | flags);  // the X launch's flags (same stream, earlier launch)
-        } else if ((MODE == 2 || MODE == 5 || MODE == 6) && a.mergeOnly) {
+        } else if (MODE == 2 && a.mergeOnly) {
             // the fused Monte-Carlo pipeline reads the flags from the merge word itself
             // (mc_survivor_kernel): no returned value to wait for
             __hip_atomic_fetch_or(&a.merge[b], flags, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1975,23 +1508,20 @@ __device__ __forceinline__ void decode_group(const BpArgs& a, const float* __res
 // past the triage, listX [0, counts[0]) then listZ [0, counts[1]), G per wave, each wave looping over
 // them (the grid does not depend on the lists' device-side lengths); merged as in split mode;
 // 3 / 4 (sector launches): sector X, then in a second launch on the same stream sector Z, of group k
-// in wave k (decode_group); 5 / 6 (list mode per sector): MODE 2 over listX alone / listZ alone, each
-// kernel compiled for its own sector.
+// in wave k (decode_group).  (List mode as two launches, one kernel per sector: -8..-12 % at
+// p = 5e-3, profiles/r05/cmp_list_sectors54_*.txt, profiles/r06/ab/cmp_occupancy_r06c.txt.)
 template <class TU, int STOP, int MODE>
 constexpr int min_waves()
 {
-    if constexpr (QEC_MIN_WAVES_PER_EU > 0) return QEC_MIN_WAVES_PER_EU;
-    if constexpr (MODE == 5) return TU::kListMinWavesX;
-    if constexpr (MODE == 6) return TU::kListMinWavesZ;
-    if constexpr (MODE == 3) return STOP != QEC_STOP_SYNDROME ? TU::kMinWavesX : TU::kSeqSynWavesX + QEC_SYN_MINW_DELTA;
-    if constexpr (MODE == 4) return STOP != QEC_STOP_SYNDROME ? TU::kMinWavesZ : TU::kSeqSynWavesZ + QEC_SYN_MINW_DELTA;
-    return STOP == QEC_STOP_SYNDROME ? TU::kMinWavesSyn + QEC_SYN_MINW_DELTA : TU::kMinWaves;
+    if constexpr (MODE == 3) return STOP != QEC_STOP_SYNDROME ? TU::kMinWavesX : TU::kSeqSynWavesX;
+    if constexpr (MODE == 4) return STOP != QEC_STOP_SYNDROME ? TU::kMinWavesZ : TU::kSeqSynWavesZ;
+    return STOP == QEC_STOP_SYNDROME ? TU::kMinWavesSyn : TU::kMinWaves;
 }
 template <int RX, int RZ, int L, int STOP, class SH, class TU, int MODE>
 __global__ __launch_bounds__(64 * waves_per_block<TU>(), (min_waves<TU, STOP, MODE>()))
 void bp_decode_kernel(const BpArgs a)
 {
-    constexpr bool LIST = MODE == 2 || MODE == 5 || MODE == 6;
+    constexpr bool LIST = MODE == 2;
     constexpr bool SPLIT = MODE == 1 || LIST;
     const int lane = threadIdx.x & 63;
     const long long wave = (long long)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
@@ -2005,11 +1535,11 @@ void bp_decode_kernel(const BpArgs a)
     const int gb = kGB ? (lane < kGB ? kGB : kGB + g * P) : g * P;
     // iteration-0 tables of both sectors (iteration0), built by the workgroup before any wave leaves
     constexpr int kTabX = (1 << RX) * RX, kTabZ = (1 << RZ) * RZ;
-    __shared__ float tab0[QEC_TABLE0 ? kTabX + kTabZ : 1];
-    if constexpr (QEC_TABLE0) {
+    __shared__ float tab0[kTabX + kTabZ];
+    {
         const float ppt = 2.0f / 3.0f * a.errorProbability;
-        if constexpr (QEC_TABLE0_HOST && kTabX + kTabZ <= kMaxTab0) {
-            (void)ppt;
+        if constexpr (kTabX + kTabZ <= kMaxTab0) {
+            (void)ppt;  // from the host (the same operations: same bits, launch_decode)
             for (int e = threadIdx.x; e < kTabX + kTabZ; e += blockDim.x) tab0[e] = a.tab0[e];
         } else {
             for (int e = threadIdx.x; e < kTabX + kTabZ; e += blockDim.x)
@@ -2017,63 +1547,26 @@ void bp_decode_kernel(const BpArgs a)
         }
         __syncthreads();
     }
-#if QEC_LIST_STAMPS
-    if (threadIdx.x < 16) stamp_lds()[threadIdx.x] = 0;
-    __syncthreads();
-    struct Flush {
-        __device__ ~Flush()
-        {
-            __syncthreads();
-            if (threadIdx.x < 16 && stamp_lds()[threadIdx.x]) atomicAdd(&g_list_stamps[threadIdx.x], stamp_lds()[threadIdx.x]);
-        }
-    } flush_stamps;
-#endif
     // this wave's decision stage for packed records (emit_decisions)
     constexpr int kStage = stage_bytes_per_wave<L, SH>();
     __shared__ __attribute__((aligned(8))) uint8_t stage_all[waves_per_block<TU>() * kStage];
     uint8_t* stage = stage_all + (threadIdx.x >> 6) * kStage;
     if constexpr (LIST) {
-        const long long nX = MODE == 6 ? 0 : a.counts[0], nZ = MODE == 5 ? 0 : a.counts[a.countStride];
+        const long long nX = a.counts[0], nZ = a.counts[a.countStride];
         const long long wXn = (nX + G - 1) / G, wTot = wXn + (nZ + G - 1) / G;
         const long long nw = (long long)gridDim.x * (blockDim.x >> 6);
-        if constexpr (!QEC_LIST_PREFETCH) {
-            for (long long vw = wave; vw < wTot; vw += nw) {
-                const bool doX = vw < wXn;  // wave-uniform
-                const long long slot = (doX ? vw : vw - wXn) * G + g;
-                const bool in_range = (g < G) && (slot < (doX ? nX : nZ));
-                const uint32_t b = in_range ? (uint32_t)(doX ? a.listX : a.listZ)[slot] : 0u;
-                // laundered per sector: the rotation addresses derived from the lane index would otherwise
-                // be hoisted out of this loop into live registers (they spilled at 3 waves per SIMD)
-                int il = i, gbl = gb;
-                asm volatile("" : "+v"(il), "+v"(gbl));
-                decode_group<RX, RZ, L, STOP, SH, StopTune<STOP, SH, TU>, MODE>(a, tab0, stage, il, gbl, b, in_range, doX);
-            }
-            return;
-        }
-        // software pipelined: the list entry two sectors ahead and the syndrome bits of the next one
-        // are in flight while a sector decodes (each is otherwise a dependent global load at its start)
-        Lane lq{i, gb, 0, 0, false};
-        auto entry = [&](long long vw, bool& dX, bool& ir) -> uint32_t {
-            dX = vw < wXn;  // wave-uniform
-            const long long slot = (dX ? vw : vw - wXn) * G + g;
-            ir = vw < wTot && (g < G) && (slot < (dX ? nX : nZ));
-            return ir ? (uint32_t)(dX ? a.listX : a.listZ)[slot] : 0u;
-        };
-        auto bits = [&](uint32_t b, bool dX, bool ir) -> uint32_t {
-            return dX ? load_sbits<RX, 0, SH>(a, lq, b, ir) : load_sbits<RZ, 1, SH>(a, lq, b, ir);
-        };
-        long long vw = wave;
-        bool dX0, ir0, dX1, ir1;
-        uint32_t b0 = entry(vw, dX0, ir0);
-        uint32_t b1 = entry(vw + nw, dX1, ir1);
-        uint32_t sb0 = bits(b0, dX0, ir0);
-        for (; vw < wTot; vw += nw) {
-            bool dX2, ir2;
-            const uint32_t b2 = entry(vw + 2 * nw, dX2, ir2);
-            const uint32_t sb1 = vw + nw < wTot ? bits(b1, dX1, ir1) : 0u;
-            decode_group<RX, RZ, L, STOP, SH, StopTune<STOP, SH, TU>, MODE>(a, tab0, stage, i, gb, b0, ir0, dX0, true, sb0);
-            b0 = b1; dX0 = dX1; ir0 = ir1; sb0 = sb1;
-            b1 = b2; dX1 = dX2; ir1 = ir2;
+        // (the next sectors' list entries and syndrome bits loaded ahead: no gain at p = 2e-3 / 5e-3, -3 %
+        // at 1e-2; round 4)
+        for (long long vw = wave; vw < wTot; vw += nw) {
+            const bool doX = vw < wXn;  // wave-uniform
+            const long long slot = (doX ? vw : vw - wXn) * G + g;
+            const bool in_range = (g < G) && (slot < (doX ? nX : nZ));
+            const uint32_t b = in_range ? (uint32_t)(doX ? a.listX : a.listZ)[slot] : 0u;
+            // laundered per sector: the rotation addresses derived from the lane index would otherwise
+            // be hoisted out of this loop into live registers (they spilled at 3 waves per SIMD)
+            int il = i, gbl = gb;
+            asm volatile("" : "+v"(il), "+v"(gbl));
+            decode_group<RX, RZ, L, STOP, SH, StopTune<STOP, SH, TU>, MODE>(a, tab0, stage, il, gbl, b, in_range, doX);
         }
         return;
     }
@@ -2100,13 +1593,7 @@ using KernelFn = void (*)(const BpArgs);
 // (profiles/r01/session7/cmp_s7u_*.txt, cmp_s7v_*.txt).  So those kernels come from there.
 // A distinct Tune type keeps the two units' kernels apart (same code, different symbols).
 // Sector launches (MODE 3 / 4, QEC_OPT_SECTOR_SPLIT = 3): X alone needs R L = 40 message registers, Z 50.
-#ifndef QEC_P61_MWX
-#define QEC_P61_MWX 6
-#endif
-#ifndef QEC_P61_MWZ
-#define QEC_P61_MWZ 5
-#endif
-using TuneP61 = Tune<5, true, false, true, true, false, true, 2, 1, 4, 1, false, QEC_P61_MWX, QEC_P61_MWZ>;
+using TuneP61 = Tune<5, true, false, true, true, false, true, 2, 1, 4, 1, false, 6, 5>;
 struct TuneP61MinReg : TuneP61 {};
 using ShiftsP61 = GeneratedShifts<4, 5, 10, 61, 9, 49, TuneP61::kRelabel, TuneP61::kMaskSelect>;
 // P7: three columns per division guard (col_group): 0.075 vs 0.077 ms at configs[1] (65 536 @ 20), even
@@ -2114,42 +1601,19 @@ using ShiftsP61 = GeneratedShifts<4, 5, 10, 61, 9, 49, TuneP61::kRelabel, TuneP6
 // P7 at 7 waves per SIMD (72 VGPRs): its fixed / reference kernels are spill-free there (8: 2-10 B of
 // scratch) at the same speed (configs[1] 0.071 vs 0.071 ms, 2^20 0.621 vs 0.618 ms;
 // profiles/r04/cmp_p7_waves.txt)
-#ifndef QEC_P7_MINW
-#define QEC_P7_MINW 7
-#endif
-#ifndef QEC_P7_MWX
-#define QEC_P7_MWX 0
-#endif
-#ifndef QEC_P7_MWZ
-#define QEC_P7_MWZ 0
-#endif
 // P7 syndrome-stop kernels at 7 waves (4 B of scratch): 6 waves are spill-free but 3-4 % slower
 // (p = 0.05 at 2^20 1.150 vs 1.111 ms; profiles/r04/cmp_p7_syndrome_waves.txt)
-#ifndef QEC_P7_SYNW
-#define QEC_P7_SYNW 7
-#endif
-using TuneP7 = Tune<QEC_P7_MINW, true, false, true, true, true, false, 2, 1, QEC_P7_SYNW, 3, false, QEC_P7_MWX, QEC_P7_MWZ>;
+using TuneP7 = Tune<7, true, false, true, true, true, false, 2, 1, 7, 3, false, 0, 0>;
 struct TuneP7MinReg : TuneP7 {};
 using ShiftsP7 = GeneratedShifts<3, 3, 6, 7, 2, 3, TuneP7::kRelabel, TuneP7::kMaskSelect>;
-#ifndef QEC_P61_MINREG
-#define QEC_P61_MINREG 1
-#endif
-#ifndef QEC_P61_SYN_MINREG
-#define QEC_P61_SYN_MINREG 0  // the P61 syndrome-stop kernels from the minreg unit too
-#endif
-#ifndef QEC_LIST_MINW_P61
-#define QEC_LIST_MINW_P61 4
-#endif
-#ifndef QEC_LIST_MINW_P7
-#define QEC_LIST_MINW_P7 5
-#endif
-using ListTuneP61 = ListTune<TuneP61, QEC_LIST_MINW_P61>;
-using ListTuneP7 = ListTune<TuneP7MinReg, QEC_LIST_MINW_P7>;
+// List mode (MODE 2): P61 at four waves per SIMD (<= 128 VGPRs; three: -5 % at p = 5e-3, -10 % at 1e-2;
+// five spill and lose 20-25 %, profiles/r05/, profiles/r06/ab/), P7 at five.
+using ListTuneP61 = ListTune<TuneP61, 4>;
+using ListTuneP7 = ListTune<TuneP7MinReg, 5>;
 KernelFn p61_minreg_kernel(int stop, bool split);  // bp_decode_p61.hip
 KernelFn p61_minreg_seq_kernel(int stop, int sec); // bp_decode_p61.hip
 KernelFn p7_minreg_kernel(int stop, bool split);   // bp_decode_p61.hip
 KernelFn p7_minreg_list_kernel();                  // bp_decode_p61.hip
-KernelFn p7_minreg_list_sec_kernel(int sec);       // bp_decode_p61.hip
 
 KernelFn phase_kernel(int P, int stop);  // bp_decode_phase.hip
 
@@ -2162,11 +1626,6 @@ KernelFn p61_minreg_kernel(int stop, bool split)
     if (stop == QEC_STOP_FIXED)
         return split ? bp_decode_kernel<4, 5, 10, QEC_STOP_FIXED, ShiftsP61, TuneP61MinReg, 1>
                      : bp_decode_kernel<4, 5, 10, QEC_STOP_FIXED, ShiftsP61, TuneP61MinReg, 0>;
-#if QEC_P61_SYN_MINREG
-    if (stop == QEC_STOP_SYNDROME)
-        return split ? bp_decode_kernel<4, 5, 10, QEC_STOP_SYNDROME, ShiftsP61, TuneP61MinReg, 1>
-                     : bp_decode_kernel<4, 5, 10, QEC_STOP_SYNDROME, ShiftsP61, TuneP61MinReg, 0>;
-#endif
     return nullptr;
 }
 KernelFn p61_minreg_seq_kernel(int stop, int sec)
@@ -2177,11 +1636,6 @@ KernelFn p61_minreg_seq_kernel(int stop, int sec)
     if (stop == QEC_STOP_FIXED)
         return sec ? bp_decode_kernel<4, 5, 10, QEC_STOP_FIXED, ShiftsP61, TuneP61MinReg, 4>
                    : bp_decode_kernel<4, 5, 10, QEC_STOP_FIXED, ShiftsP61, TuneP61MinReg, 3>;
-#if QEC_SEQ_SYN_MINREG
-    if (stop == QEC_STOP_SYNDROME)
-        return sec ? bp_decode_kernel<4, 5, 10, QEC_STOP_SYNDROME, ShiftsP61, SeqSynTune<TuneP61MinReg>, 4>
-                   : bp_decode_kernel<4, 5, 10, QEC_STOP_SYNDROME, ShiftsP61, SeqSynTune<TuneP61MinReg>, 3>;
-#endif
     return nullptr;
 }
 KernelFn p7_minreg_kernel(int stop, bool split)
@@ -2192,11 +1646,6 @@ KernelFn p7_minreg_kernel(int stop, bool split)
     return nullptr;
 }
 KernelFn p7_minreg_list_kernel() { return bp_decode_kernel<3, 3, 6, QEC_STOP_SYNDROME, ShiftsP7, ListTuneP7, 2>; }
-KernelFn p7_minreg_list_sec_kernel(int sec)
-{
-    return sec ? bp_decode_kernel<3, 3, 6, QEC_STOP_SYNDROME, ShiftsP7, ListTuneP7, 6>
-               : bp_decode_kernel<3, 3, 6, QEC_STOP_SYNDROME, ShiftsP7, ListTuneP7, 5>;
-}
 #elif defined(QEC_PHASE_TU)
 // The instrumented kernels of the shipped codes (QEC_OPT_PHASE_STATS, one wave per syndrome):
 // iters[] reports per sector soft | hard << 8 | agreed << 16 | jumped << 24 iterations.
@@ -2224,13 +1673,11 @@ struct Variant {
     KernelFn fn[3];     // indexed by stop rule
     KernelFn split[3];  // the same with one wave per sector (nullptr: not instantiated)
     KernelFn phase[3];  // QEC_OPT_PHASE_STATS: instrumented kernels (shipped codes only)
-    int (*fill_tab0)(float pp, float* out);  // host iteration-0 tables (QEC_TABLE0_HOST)
+    int (*fill_tab0)(float pp, float* out);  // host iteration-0 tables (kernel arguments)
     uint32_t (*zero_out[2])(float pp, int N, int stop);  // per sector: zero-syndrome outcomes (zero_outcome)
     const char* name;
     KernelFn list = nullptr;  // syndrome stop, list mode (MODE 2: the sectors the triage passed on)
     int min_waves_syn = 1;    // its occupancy (waves per SIMD), for the list launch's grid
-    KernelFn list_sec[2] = {};        // the same per sector (MODE 5 / 6; QEC_LIST_SECTORS)
-    int list_waves[2] = {1, 1};       // their occupancies
     KernelFn seq[3][2] = {};     // sector launches (MODE 3 / 4): [stop][sector]
     // QEC_OPT_SECTOR_SPLIT = 1 takes the sector launches from this batch on, per stop rule (0: never), and
     // under the syndrome stop only from seq_syn_min_p on
@@ -2276,12 +1723,6 @@ static Variant make_variant(int P, int S, int T, const char* name)
         v.seq[QEC_STOP_SYNDROME][1] = bp_decode_kernel<J, K, L, QEC_STOP_SYNDROME, SH, SeqSynTune<TU>, 4>;
     }
     v.min_waves_syn = TUL::kMinWavesSyn;  // the list launch's grid (launch_decode_list)
-    if constexpr (WITH_SPLIT) {
-        v.list_sec[0] = bp_decode_kernel<J, K, L, QEC_STOP_SYNDROME, SH, TUL, 5>;
-        v.list_sec[1] = bp_decode_kernel<J, K, L, QEC_STOP_SYNDROME, SH, TUL, 6>;
-        v.list_waves[0] = TUL::kListMinWavesX;
-        v.list_waves[1] = TUL::kListMinWavesZ;
-    }
     return v;
 }
 // Tune<min waves per SIMD, relabel, zero-skip, short division, hard-message paths, sector split,
@@ -2313,20 +1754,20 @@ static Variant gen()
 // the agreement test (kAgree) the syndrome-stop kernels are spill-free, P61 at 4 waves (125 VGPRs)
 // and P7 at 7 (with the lane relabelling and gather pipelining P7 now takes too, 2-5 % faster
 // at every stop rule: 260 instead of 456 static ds_bpermute; profiles/r02/p7_variants_r02s3{s,t}.txt).
-// With the iteration-0 tables from the host (QEC_TABLE0_HOST) nothing is shared between the waves
+// With the iteration-0 tables from the host nothing is shared between the waves
 // of a workgroup any more, and one-wave workgroups are fastest for both codes (P61 headline 134.0
 // vs 131.9M syn/s with two, P7 +3 % vs four; profiles/r02/cmp_wpb_r02s3x.txt).
 static Variant gen_p61()
 {
     Variant v = gen<4, 5, 10, 61, 9, 49, TuneP61, ListTuneP61>();
     for (int stop : {QEC_STOP_REF, QEC_STOP_FIXED, QEC_STOP_SYNDROME}) v.phase[stop] = phase_kernel(61, stop);
-    if (QEC_P61_MINREG) {
-        for (int stop : {QEC_STOP_REF, QEC_STOP_FIXED, QEC_STOP_SYNDROME}) {
-            if (stop == QEC_STOP_SYNDROME && !QEC_P61_SYN_MINREG) continue;
+    {
+        // the reference- and fixed-stop kernels from the minreg unit (the syndrome stop's spill more there;
+        // its sector launches measured +-0, profiles/r05/cmp_syn_seq_waves_*.txt)
+        for (int stop : {QEC_STOP_REF, QEC_STOP_FIXED}) {
             v.fn[stop] = p61_minreg_kernel(stop, false);
             v.split[stop] = p61_minreg_kernel(stop, true);
-            if (stop != QEC_STOP_SYNDROME || QEC_SEQ_SYN_MINREG)
-                for (int sec = 0; sec < 2; ++sec) v.seq[stop][sec] = p61_minreg_seq_kernel(stop, sec);
+            for (int sec = 0; sec < 2; ++sec) v.seq[stop][sec] = p61_minreg_seq_kernel(stop, sec);
         }
         // sector launches, fixed stop from 2^18 syndromes on: +1.3 % at 262 144, +0.3 % at 524 288, +1.9 % at
         // 2^20, but -2.7 % at 131 072 and -10 % at 65 536 (a second launch tail; profiles/r04/cmp_sector_launch_*.txt);
@@ -2345,15 +1786,10 @@ static Variant gen_p7()
 {
     Variant v = gen<3, 3, 6, 7, 2, 3, TuneP7, ListTuneP7>();
     for (int stop : {QEC_STOP_REF, QEC_STOP_FIXED, QEC_STOP_SYNDROME}) v.phase[stop] = phase_kernel(7, stop);
-    if (QEC_P61_MINREG) {
-        v.fn[QEC_STOP_SYNDROME] = p7_minreg_kernel(QEC_STOP_SYNDROME, false);
-        v.split[QEC_STOP_SYNDROME] = p7_minreg_kernel(QEC_STOP_SYNDROME, true);
-        v.list = p7_minreg_list_kernel();
-        v.min_waves_syn = ListTuneP7::kMinWavesSyn;
-        for (int sec = 0; sec < 2; ++sec) v.list_sec[sec] = p7_minreg_list_sec_kernel(sec);
-        v.list_waves[0] = ListTuneP7::kListMinWavesX;
-        v.list_waves[1] = ListTuneP7::kListMinWavesZ;
-    }
+    v.fn[QEC_STOP_SYNDROME] = p7_minreg_kernel(QEC_STOP_SYNDROME, false);
+    v.split[QEC_STOP_SYNDROME] = p7_minreg_kernel(QEC_STOP_SYNDROME, true);
+    v.list = p7_minreg_list_kernel();
+    v.min_waves_syn = ListTuneP7::kMinWavesSyn;
     return v;
 }
 
@@ -2486,8 +1922,8 @@ int launch_decode(const void* variant, const Code& c, const uint8_t* sX, const u
     a.stop = stop;
     a.hardPaths = hardPaths & (QEC_HP_FORMS | QEC_HP_CYCLE);
     a.scaled = scaled_ok(2.0f / 3.0f * errorProbability) ? 1 : 0;
-    if (QEC_TABLE0_HOST) v->fill_tab0(2.0f / 3.0f * errorProbability, a.tab0);  // p' as the kernel forms it
-    if (QEC_ZERO_OUTCOME && !phase)
+    v->fill_tab0(2.0f / 3.0f * errorProbability, a.tab0);  // p' as the kernel forms it
+    if (!phase)
         for (int sec = 0; sec < 2; ++sec) a.zs[sec] = v->zero_out[sec](2.0f / 3.0f * errorProbability, a.maxIter, stop);
     relabel(c.EX.data(), c.J, c.L, c.P, v->relabel, a.SX, a.DX, a.CX);
     relabel(c.EZ.data(), c.K, c.L, c.P, v->relabel, a.SZ, a.DZ, a.CZ);
@@ -2515,20 +1951,6 @@ int launch_decode(const void* variant, const Code& c, const uint8_t* sX, const u
 
 bool decode_has_list(const void* variant) { return static_cast<const Variant*>(variant)->list != nullptr; }
 
-#if QEC_LIST_STAMPS
-}  // namespace qec
-// experiment builds: copies the 16 stamp words to out (host) and, with reset, zeroes them
-extern "C" int qec_debug_list_stamps(unsigned long long* out, int reset)
-{
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(qec::g_list_stamps), sizeof(unsigned long long) * 16) != hipSuccess) return 1;
-    if (reset) {
-        static const unsigned long long zero[16] = {};
-        if (hipMemcpyToSymbol(HIP_SYMBOL(qec::g_list_stamps), zero, sizeof zero) != hipSuccess) return 1;
-    }
-    return 0;
-}
-namespace qec {
-#endif
 
 // Compute units of the current device (4 SIMDs each), cached per device (the list-mode grid).
 static int device_cus()
@@ -2590,7 +2012,7 @@ int launch_decode_list(const void* variant, const Code& c, const uint8_t* sX, co
     a.sX = sX; a.sZ = sZ; a.sbits = 1;
     a.wX = (c.mX + 31) / 32; a.wZ = (c.mZ + 31) / 32;
     a.rec = rec; a.iters = iters; a.merge = merge;
-    a.listX = listX; a.listZ = listZ; a.counts = counts; a.mergeOnly = QEC_LIST_MERGE_ONLY && merge_only ? 1 : 0;
+    a.listX = listX; a.listZ = listZ; a.counts = counts; a.mergeOnly = merge_only ? 1 : 0;
     a.countStride = count_stride;
     a.B = B; a.P = c.P; a.G = 64 / c.P;
     a.n = c.n; a.mX = c.mX; a.mZ = c.mZ;
@@ -2600,32 +2022,20 @@ int launch_decode_list(const void* variant, const Code& c, const uint8_t* sX, co
     a.stop = QEC_STOP_SYNDROME;
     a.hardPaths = hardPaths & (QEC_HP_FORMS | QEC_HP_CYCLE);
     a.scaled = scaled_ok(2.0f / 3.0f * errorProbability) ? 1 : 0;
-    if (QEC_TABLE0_HOST) v->fill_tab0(2.0f / 3.0f * errorProbability, a.tab0);
+    v->fill_tab0(2.0f / 3.0f * errorProbability, a.tab0);
     relabel(c.EX.data(), c.J, c.L, c.P, v->relabel, a.SX, a.DX, a.CX);
     relabel(c.EZ.data(), c.K, c.L, c.P, v->relabel, a.SZ, a.DZ, a.CZ);
-    static const long long rounds = [] {  // QEC_LIST_ROUNDS: grid in resident-slot rounds (experiments)
-        const char* e = std::getenv("QEC_LIST_ROUNDS");
-        const int v = e ? std::atoi(e) : 0;
-        return (long long)(v >= 1 && v <= 64 ? v : 1);
-    }();
+    // one wave per resident slot of the chip (more rounds of the grid measured no gain,
+    // profiles/r03/list_rounds/), each looping over the listed sectors
     const int wpb = v->waves_per_block;
-    auto launch = [&](KernelFn fn, long long need, int waves_per_simd) -> int {
-        const long long cap = 4LL * device_cus() * waves_per_simd * rounds;  // one per resident slot of the chip
-        const long long waves = need < cap ? need : cap;
-        const long long blocks = (waves + wpb - 1) / wpb;
-        hipLaunchKernelGGL(fn, dim3((unsigned)blocks), dim3(64 * wpb), 0, stream, a);
-        const hipError_t err = hipGetLastError();
-        if (err != hipSuccess) return fail(QEC_ERR_HIP, std::string("bp_decode list launch: ") + hipGetErrorString(err));
-        return QEC_OK;
-    };
-    if (QEC_LIST_SECTORS && v->list_sec[0] && v->list_sec[1]) {
-        // listX in a kernel compiled for sector X alone, then listZ (the two merge their flags in the
-        // merge words, in either order)
-        const long long need = (B + a.G - 1) / a.G;  // waves for every sector of one list
-        const int rc = launch(v->list_sec[0], need, v->list_waves[0]);
-        return rc ? rc : launch(v->list_sec[1], need, v->list_waves[1]);
-    }
-    return launch(v->list, (2 * B + a.G - 1) / a.G, v->min_waves_syn);
+    const long long need = (2 * B + a.G - 1) / a.G;
+    const long long cap = 4LL * device_cus() * v->min_waves_syn;
+    const long long waves = need < cap ? need : cap;
+    const long long blocks = (waves + wpb - 1) / wpb;
+    hipLaunchKernelGGL(v->list, dim3((unsigned)blocks), dim3(64 * wpb), 0, stream, a);
+    const hipError_t err = hipGetLastError();
+    if (err != hipSuccess) return fail(QEC_ERR_HIP, std::string("bp_decode list launch: ") + hipGetErrorString(err));
+    return QEC_OK;
 }
 
 #endif  // QEC_P61_MINREG_TU / QEC_PHASE_TU

@@ -447,9 +447,6 @@ __global__ __launch_bounds__(64 * kGapWaves) void mc_gap_kernel(const GapArgs a)
 // needs the I-P columns (no syndrome failure, nonzero residual).  NJ = 0: any code, one sample at
 // a time.
 constexpr int kMaxRecWords = 80;  // 2 nb <= 640 bytes
-#ifndef QEC_STAT_U
-#define QEC_STAT_U 4
-#endif
 
 template <int NJ, int U>
 __global__ __launch_bounds__(64 * kStatBlockWaves) void statistics_packed_kernel(
@@ -519,190 +516,6 @@ __global__ __launch_bounds__(64 * kStatBlockWaves) void statistics_packed_kernel
     stat_flush(part, c, iters != nullptr ? C_N + 2 : C_N, counters);
 }
 
-// The same counters with one lane per sample (statistics_rows_kernel).  A wave takes S consecutive
-// samples: their packed-error rows and decision records are two contiguous byte ranges, copied into
-// the wave's LDS with 16-byte loads (the kernel above loads one byte per lane: 64 B per wave
-// instruction, latency-bound at ~1.4 TB/s).  Lane s then reads sample s's rows as dwords (byte
-// alignment by funnel shift), ORs its x, z and residual bytes, and the wave adds its samples' 0/1
-// outcomes with ballot popcounts (scalar).  The rare sample needing the I-P columns (no syndrome
-// failure, nonzero residual) has its residual words formed by the wave in LDS and goes through
-// logical_from_columns, one at a time.
-constexpr int kRowWaves = 4;          // waves per workgroup
-constexpr int kRowLdsPerWave = 10304;  // bytes: S (estride + recB) + 2 x 16 of alignment slack, S <= 32 (P61: 9 984)
-
-// bytes [src, src + nb) of global memory into LDS at dst + (src & 15), for two ranges at once:
-// 16-byte loads over the aligned bodies -- every load of both bodies issued before the first LDS
-// store (up to 8 per lane in flight), single bytes for the unaligned heads and tails (nothing
-// outside the ranges is read)
-struct StageRange {
-    uint8_t* dst;
-    const uint8_t* src;
-    int nb;
-    uintptr_t a0, b0, b1;
-    int head, tail, nv;
-    __device__ __forceinline__ StageRange(uint8_t* d, const uint8_t* s, int n) : dst(d), src(s), nb(n)
-    {
-        const uintptr_t s0 = reinterpret_cast<uintptr_t>(s), s1 = s0 + (uintptr_t)n;
-        a0 = s0 & ~(uintptr_t)15;
-        b0 = (s0 + 15) & ~(uintptr_t)15;
-        b1 = s1 & ~(uintptr_t)15;
-        if (b0 > b1) b0 = b1 = s1;  // the whole range inside one 16-byte line: bytes only
-        head = (int)(b0 - s0);
-        tail = (int)(s1 - b1);
-        nv = (int)((b1 - b0) >> 4);
-    }
-    __device__ __forceinline__ void ends(int lane) const
-    {
-        const uintptr_t s0 = reinterpret_cast<uintptr_t>(src);
-        if (lane < head) dst[(s0 - a0) + lane] = src[lane];
-        if (lane < tail) dst[(b1 - a0) + lane] = *reinterpret_cast<const uint8_t*>(b1 + lane);
-    }
-};
-
-__device__ __forceinline__ void stage_two(const StageRange& x, const StageRange& y, int lane)
-{
-    constexpr int kMaxPer = 8;  // 16-byte loads per lane and range in flight
-    x.ends(lane);
-    y.ends(lane);
-    const uint4* __restrict__ gx = reinterpret_cast<const uint4*>(x.b0);
-    const uint4* __restrict__ gy = reinterpret_cast<const uint4*>(y.b0);
-    uint4* __restrict__ lx = reinterpret_cast<uint4*>(x.dst + (x.b0 - x.a0));
-    uint4* __restrict__ ly = reinterpret_cast<uint4*>(y.dst + (y.b0 - y.a0));
-    const int n = x.nv > y.nv ? x.nv : y.nv;
-    for (int base = 0; base < n; base += 64 * kMaxPer) {
-        uint4 vx[kMaxPer], vy[kMaxPer];
-#pragma unroll
-        for (int k = 0; k < kMaxPer; ++k) {
-            const int t = base + lane + 64 * k;
-            if (t < x.nv) vx[k] = gx[t];
-            if (t < y.nv) vy[k] = gy[t];
-        }
-#pragma unroll
-        for (int k = 0; k < kMaxPer; ++k) {
-            const int t = base + lane + 64 * k;
-            if (t < x.nv) lx[t] = vx[k];
-            if (t < y.nv) ly[t] = vy[k];
-        }
-    }
-}
-
-// dword k (bytes 4k .. 4k + 3) of a row starting at any byte offset o of the stage
-__device__ __forceinline__ uint32_t row_word(const uint8_t* __restrict__ stage, int o, int k)
-{
-    const int a = o + 4 * k, w = a & ~3, sh = a & 3;
-    const uint32_t lo = *reinterpret_cast<const uint32_t*>(stage + w);
-    if (sh == 0) return lo;
-    const uint32_t hi = *reinterpret_cast<const uint32_t*>(stage + w + 4);
-    return __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)sh);
-}
-
-__global__ __launch_bounds__(64 * kRowWaves) void statistics_rows_kernel(
-    const uint8_t* __restrict__ errp, int estride, const uint8_t* __restrict__ rec, const int32_t* __restrict__ iters,
-    long long B, int n, int nb, int S, const uint64_t* __restrict__ imp_cols, int imp_cw,
-    unsigned long long* __restrict__ counters)
-{
-    extern __shared__ __attribute__((aligned(16))) uint8_t row_smem[];
-    __shared__ unsigned long long part[kRowWaves][C_N + 2];
-    __shared__ unsigned long long sres[kRowWaves][kMaxRecWords];
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int recB = 2 * nb + 1, eb = 2 * nb;
-    const int ewords = (eb + 3) / 4;  // dwords covering a row's decision bytes
-    uint8_t* __restrict__ est = row_smem + (size_t)wv * kRowLdsPerWave;
-    uint8_t* __restrict__ rst = est + ((S * estride + 16 + 15) & ~15);
-    unsigned long long c[C_N] = {};
-    unsigned long long itx = 0, itz = 0;  // this lane's iteration sums
-    const long long step = (long long)gridDim.x * kRowWaves * S;
-    for (long long b0 = ((long long)blockIdx.x * kRowWaves + wv) * S; b0 < B; b0 += step) {
-        const int ns = (int)(B - b0 < S ? B - b0 : S);
-        const uint8_t* ge = errp + b0 * estride;
-        const uint8_t* gr = rec + b0 * recB;
-        stage_two(StageRange(est, ge, ns * estride), StageRange(rst, gr, ns * recB), lane);
-        const bool valid = lane < ns;
-        if (iters != nullptr && valid) {
-            itx += (unsigned)iters[2 * (b0 + lane)];
-            itz += (unsigned)iters[2 * (b0 + lane) + 1];
-        }
-        wave_sync();
-        const int oe = (int)(reinterpret_cast<uintptr_t>(ge) & 15) + lane * estride;
-        const int orr = (int)(reinterpret_cast<uintptr_t>(gr) & 15) + lane * recB;
-        uint32_t ax = 0, az = 0, ar = 0;
-        if (valid) {
-            for (int k = 0; k < ewords; ++k) {
-                // byte masks of this word: x bytes [0, nb), z bytes [nb, 2 nb) (wave-uniform)
-                const int bx = nb - 4 * k, bz = eb - 4 * k;
-                const uint32_t mx = bx >= 4 ? ~0u : bx <= 0 ? 0u : (1u << (8 * bx)) - 1u;
-                const uint32_t mall = bz >= 4 ? ~0u : bz <= 0 ? 0u : (1u << (8 * bz)) - 1u;
-                const uint32_t e = row_word(est, oe, k), r = row_word(rst, orr, k);
-                ax |= e & mx;
-                az |= e & mall & ~mx;
-                ar |= (e ^ r) & mall;
-            }
-        }
-        const uint32_t f = valid ? rst[orr + eb] : 0u;
-        const bool dEX = (f & QEC_SYNDROME_FAIL_X) != 0, dEZ = (f & QEC_SYNDROME_FAIL_Z) != 0;
-        // samples needing the I-P columns: no syndrome failure, nonzero residual (the decoder found
-        // something else than the error)
-        unsigned long long need = __ballot(valid && !(dEX || dEZ) && ar != 0u);
-        unsigned long long logical = 0;
-        if (imp_cw > 0) {
-            const int nw = (eb + 7) / 8;  // 64-bit residual words (record layout)
-            while (need) {
-                const int s = __builtin_ctzll(need);
-                need &= need - 1;
-                const int oe_s = (int)(reinterpret_cast<uintptr_t>(ge) & 15) + s * estride;
-                const int or_s = (int)(reinterpret_cast<uintptr_t>(gr) & 15) + s * recB;
-                if (lane < nw) {
-                    uint64_t w = 0;
-                    for (int j = 0; j < 8; ++j) {
-                        const int t = 8 * lane + j;
-                        const uint64_t by = t < eb ? (uint64_t)(est[oe_s + t] ^ rst[or_s + t]) : 0ull;
-                        w |= by << (8 * j);
-                    }
-                    sres[wv][lane] = w;
-                }
-                wave_sync();
-                if (logical_from_columns<true>(sres[wv], nw, n, nb, imp_cols, imp_cw, lane)) logical |= 1ull << s;
-                wave_sync();
-            }
-        }
-        const unsigned long long vm = __ballot(valid), sx = __ballot(dEX), sz = __ballot(dEZ);
-        const unsigned long long ok = vm & ~(sx | sz);
-        c[C_WITHX] += __popcll(__ballot(ax != 0u));
-        c[C_WITHZ] += __popcll(__ballot(az != 0u));
-        c[C_SYNX] += __popcll(sx);
-        c[C_SYNZ] += __popcll(sz);
-        c[C_LOGICAL] += __popcll(ok & logical);
-        c[C_CORRECTED] += __popcll(ok & ~logical);
-        c[C_CONVX] += __popcll(__ballot((f & QEC_CONVERGENCE_FAIL_X) != 0));
-        c[C_CONVZ] += __popcll(__ballot((f & QEC_CONVERGENCE_FAIL_Z) != 0));
-        wave_sync();  // the stage is reused by the next chunk
-    }
-    // iteration sums: wave reduction of the per-lane values
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) {
-        itx += __shfl_xor(itx, o);
-        itz += __shfl_xor(itz, o);
-    }
-    unsigned long long cc[C_N + 2];
-#pragma unroll
-    for (int k = 0; k < C_N; ++k) cc[k] = c[k];
-    cc[C_N] = itx;
-    cc[C_N + 1] = itz;
-    // stat_flush with kRowWaves waves
-    if (lane < C_N + 2) {
-        unsigned long long v = 0;
-#pragma unroll
-        for (int k = 0; k < C_N + 2; ++k) v = lane == k ? cc[k] : v;
-        part[wv][lane] = v;
-    }
-    __syncthreads();
-    const int nc = iters != nullptr ? C_N + 2 : C_N;
-    if (threadIdx.x < nc) {
-        unsigned long long v = 0;
-        for (int w = 0; w < kRowWaves; ++w) v += part[w][threadIdx.x];
-        if (v) atomicAdd(&counters[threadIdx.x], v);
-    }
-}
 
 // The counters with one lane per sample reading its two rows straight from global memory (no LDS
 // stage): packed errors and records at word-aligned row strides (the Monte-Carlo pipeline's
@@ -841,15 +654,9 @@ static uint32_t magic_of(long long d) { return d > 1 ? (uint32_t)(((1ull << 32) 
 // 16 and 64 -- a wave's walk lasts as long as its busiest lane, so more samples per wave cost less
 // per sample once there are enough waves (P61, 2^20 samples: 206 / 126 / 124 us at 16 / 32 / 64 per
 // wave at p = 0.002, 1109 / 542 us at 16 / 64 at p = 0.05; 65 536 samples: 16 best, 20 vs 22 us at
-// 64; profiles/r02/gap_spw_r02s3zn.txt).  QEC_GAP_SPW overrides, for experiments.
+// 64; profiles/r02/gap_spw_r02s3zn.txt).
 static int gap_spw(long long B)
 {
-    static const int v = [] {
-        const char* e = std::getenv("QEC_GAP_SPW");
-        const int k = e ? std::atoi(e) : 0;
-        return k >= 1 && k <= 64 ? k : 0;
-    }();
-    if (v) return v;
     int spw = 16;
     while (spw < 64 && B / (2 * spw) >= 8192) spw *= 2;
     return spw;
@@ -974,24 +781,11 @@ int launch_statistics_packed(const Code& c, const uint64_t* imp_cols, const uint
         return fail(QEC_ERR_UNSUPPORTED, "packed statistics: padded record rows need the lane kernel");
     if ((2 * nb + 7) / 8 > kMaxRecWords || c.imp_col_words > 64)
         return fail(QEC_ERR_UNSUPPORTED, "packed statistics kernel: code too long");
-    // the LDS-staged row kernel (unaligned public layout) measured slower than the byte kernel below at
-    // P61 (195-304 vs 231 us per 2^20, profiles/r03/): experiments only
-    static const int rows = [] { const char* e = std::getenv("QEC_STAT_ROWS"); return e ? std::atoi(e) : 0; }();
-    if (rows) {
-        int S = 32;
-        while (S >= 8 && S * (estride + 2 * nb + 1) + 64 > kRowLdsPerWave) S /= 2;
-        if (S >= 8) {
-            static const int maxb = [] { const char* e = std::getenv("QEC_STAT_BLOCKS"); const int v = e ? std::atoi(e) : 0; return v > 0 ? v : 1024; }();
-            const long long blocks = std::min<long long>((B + kRowWaves * S - 1) / (kRowWaves * S), maxb);
-            hipLaunchKernelGGL(statistics_rows_kernel, dim3((unsigned)blocks), dim3(64 * kRowWaves),
-                               (size_t)kRowWaves * kRowLdsPerWave, st, errp, estride, rec, iters, B, c.n, nb, S, imp_cols,
-                               c.imp_col_words, counters);
-            return launch_check("statistics_rows");
-        }
-    }
+    // (an LDS-staged row kernel measured slower than the byte kernel below at P61: 195-304 vs 231 us per
+    // 2^20, profiles/r03/)
     const int nj = (8 * ((2 * nb + 7) / 8) + 63) / 64;
-    constexpr int U = QEC_STAT_U;
-    static const int maxb = [] { const char* e = std::getenv("QEC_STAT_BLOCKS"); const int v = e ? std::atoi(e) : 0; return v > 0 ? v : kStatMaxBlocks; }();
+    constexpr int U = 4;
+    constexpr int maxb = kStatMaxBlocks;
     const long long blocks = std::min<long long>((B + kStatBlockWaves * U - 1) / (kStatBlockWaves * U), maxb);
     auto kern = nj == 1 ? statistics_packed_kernel<1, U> : nj == 3 ? statistics_packed_kernel<3, U> : statistics_packed_kernel<0, 1>;
     hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(64 * kStatBlockWaves), 0, st, errp, estride, rec, iters, B,

@@ -39,25 +39,15 @@ constexpr int kBuckets = 256;    // bucket k = 255 - min(weight, 255): 0 = heavi
 constexpr int kHistThreads = 1024;
 // threads per syndrome in the weight pass: 4 for long rows (P61: 549 bytes), 1 for short ones
 // (P7: 42 bytes), where four threads would only multiply the waves of a latency-bound launch
-// (QEC_HIST_SPLIT = 8, one round of loads per thread for P61, is slower: 23.8 vs 17.1 us,
+// (8, one round of loads per thread for P61, is slower: 23.8 vs 17.1 us,
 // profiles/r01/session7/rocprof_hist_split_s7bb.csv)
-#ifndef QEC_HIST_SPLIT
-#define QEC_HIST_SPLIT 4
-#endif
-constexpr int kHistSplitLong = QEC_HIST_SPLIT;
+constexpr int kHistSplitLong = 4;
 constexpr int kShortRows = 128;  // mX + mZ up to this many bytes: one thread per syndrome
 constexpr int kMaxChunks = 1024;
 constexpr int kMaxChunk = 4096;
-#ifndef QEC_SCHED_FUSED_MAX
-#define QEC_SCHED_FUSED_MAX 256  // experiments: 0 always takes the separate offsets pass
-#endif
-#ifndef QEC_SCHED_SECTORS
-#define QEC_SCHED_SECTORS 1  // sector-split launches: each sector's waves in the order of that sector's weight
-#endif
-constexpr bool kSchedSectors = QEC_SCHED_SECTORS;
-#ifndef QEC_SCHED_TARGET_CHUNKS
-#define QEC_SCHED_TARGET_CHUNKS 128  // chunks (histogram workgroups) aimed for when the batch is small
-#endif
+// sector-split launches: each sector's waves in the order of that sector's weight
+constexpr bool kSchedSectors = true;
+constexpr int kTargetChunks = 128;  // chunks (histogram workgroups) aimed for when the batch is small
 
 // Weight (bit 0 of each byte) of bytes [g0, g1) of s, read by one thread with 16-byte loads at
 // aligned addresses; bytes outside the range are masked off (the first and last loads may
@@ -227,7 +217,7 @@ __global__ __launch_bounds__(kScatThreads) void schedule_scatter_kernel(const ui
 // three passes 46 us, of which the 16-workgroup histogram 36 us, profiles/r03/).  It also sizes the
 // buckets to the largest possible weight (P7: mX + mZ + 1 = 43 instead of 256: the count matrix
 // each workgroup reads shrinks with them).
-constexpr int kMaxFusedChunks = QEC_SCHED_FUSED_MAX;
+constexpr int kMaxFusedChunks = 256;
 struct FusedLds {
     uint32_t tot[kScatThreads], pre[kScatThreads];  // [part][bucket], part * nbk + k = t
     uint32_t start[kBuckets];
@@ -284,7 +274,7 @@ __global__ __launch_bounds__(kScatThreads) void schedule_scatter_fused_kernel(co
     scatter_fused_body(key, B, chunk, nch, nbk, counts, perm, s, blockIdx.x);
 }
 
-// Per-sector order (QEC_SCHED_SECTORS, the sector-split launch): an X wave's work depends on the X
+// Per-sector order (kSchedSectors, the sector-split launch): an X wave's work depends on the X
 // sector's weight alone and a Z wave's on the Z sector's, so each sector gets its own heaviest-first
 // order -- perm[0, B) for the X waves, perm[B, 2 B) for the Z waves -- from its own keys and counts
 // (X and Z in one histogram pass; the scatter's first nch workgroups place X, the others Z).  P7
@@ -499,23 +489,14 @@ __global__ __launch_bounds__(kLocalThreads) void schedule_local_kernel(const uin
 
 // rows per chunk: at least min_chunk (one pass of the histogram workgroup), enough that there
 // are at most kMaxChunks chunks
-// and, below that, about QEC_SCHED_TARGET_CHUNKS chunks (power-of-two sizes up to max_chunk), so a small
+// and, below that, about kTargetChunks chunks (power-of-two sizes up to max_chunk), so a small
 // batch still spreads its histogram over many workgroups (P7 65 536 at the fixed 4096 rows per chunk:
 // 16 workgroups, 36 us)
 static int chunk_of(long long B, int min_chunk, int max_chunk, int* nchunks)
 {
-    static const int forced = [] {  // QEC_SCHED_CHUNK: rows per chunk, for experiments
-        const char* e = std::getenv("QEC_SCHED_CHUNK");
-        const int v = e ? std::atoi(e) : 0;
-        return v >= 64 && v <= kMaxChunk ? v : 0;
-    }();
-    if (forced && (B + forced - 1) / forced <= kMaxChunks) {
-        *nchunks = (int)((B + forced - 1) / forced);
-        return forced;
-    }
     long long chunk = (B + kMaxChunks - 1) / kMaxChunks;
     long long want = min_chunk;
-    while (want < max_chunk && want * QEC_SCHED_TARGET_CHUNKS < B) want *= 2;
+    while (want < max_chunk && want * kTargetChunks < B) want *= 2;
     if (chunk < want) chunk = want;
     *nchunks = (int)((B + chunk - 1) / chunk);
     return (int)chunk;

@@ -531,6 +531,18 @@ __device__ __forceinline__ void check_pass_hard(float (&msg)[R][L], uint32_t sbi
     }
 }
 
+// The hard decision of one variable (DecoderCPU.h:354-373): some of its R messages q >= 0.5f.  (As the
+// maximum of the R messages by v_max3_f32 -- NaN-safe, the messages are probabilities or quiet NaNs --
+// and one compare: -0.6 .. +1.1 % on config 5, profiles/r06/ab/cmp_hd_max.txt; not taken.)
+template <int R>
+__device__ __forceinline__ bool any_ge_half(const float (&q)[R])
+{
+    bool hd = false;
+#pragma unroll
+    for (int r = 0; r < R; ++r) hd |= (q[r] >= 0.5f);
+    return hd;
+}
+
 // Zero numerators.  A numerator n = +0 is harmless: then d = P0 = (1 - p') prod (1 - g_k) over F
 // factors, where every 1 - g_k is exact and either 0 or >= 2^-24 (g <= 1 - 2^-24 when g < 1), so
 // d is either 0 (0 / 0: NaN from both sequences) or >= (1 - p') 2^(-24 F), which for p' <= 1/2 and
@@ -746,17 +758,19 @@ __device__ __forceinline__ uint32_t var_pass(const BpArgs& a, float (&msg)[R][L]
 #pragma unroll
         for (int c = 0; c < CG; ++c) {
             const int l = l0 + c;
-            if constexpr (HD) {
-                bool hd = false;
-#pragma unroll
-                for (int r = 0; r < R; ++r) hd |= (qv[c][r] >= 0.5f);
-                hdmask |= (uint32_t)hd << l;
-            }
+            if constexpr (HD) hdmask |= (uint32_t)any_ge_half<R>(qv[c]) << l;
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 const int sh = SH::template shift<SEC, L>(et, r, l);
                 msg[r][l] = defer_return<HD, SH>() ? qv[c][r] : rot<SH>(qv[c][r], ln, sh == 0 ? 0 : P - sh);
             }
+        }
+        if constexpr (TU::kSaturate) {
+            // a soft output in the first column group already decides that the sector does not turn hard in
+            // this pass: the remaining columns skip the hard-state test (its fma and OR per message, compare
+            // per variable), which otherwise costs ~9 % of a soft pass (headline +1.1 %, 50 fixed iterations
+            // at p = 0.1 +7.7 %, P7 +2.6 %; profiles/r06/ab/cmp_track_early.txt)
+            if (l0 == 0 && track && !all_live_sh<SH>(soft_bits == 0u, ln.live)) track = false;
         }
         // a scheduling barrier after each column group: the machine scheduler otherwise hoists work
         // across columns into more live registers (P61 headline +2.8 %, profiles/r03/cmp_col_barrier_*.txt)
@@ -1067,12 +1081,7 @@ __device__ __forceinline__ bool iteration0(const BpArgs& a, float (&msg)[R][L], 
         float qv[R];
 #pragma unroll
         for (int r = 0; r < R; ++r) qv[r] = tab[idx * R + r];
-        if constexpr (HD) {
-            bool hd = false;
-#pragma unroll
-            for (int r = 0; r < R; ++r) hd |= (qv[r] >= 0.5f);
-            hdmask |= (uint32_t)hd << l;
-        }
+        if constexpr (HD) hdmask |= (uint32_t)any_ge_half<R>(qv) << l;
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             const int sh = SH::template shift<SEC, L>(et, r, l);

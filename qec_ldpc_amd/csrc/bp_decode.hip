@@ -92,10 +92,13 @@ struct SeqSynTune : TU {
     static constexpr int kSeqSynWavesX = 5 > TU::kMinWavesSyn ? 5 : TU::kMinWavesSyn;
 };
 
-// The list-mode (MODE 2) tuning of a variant: its own occupancy (no agreement test, no cycle jump).
-template <class TU, int LW>
+// The list-mode (MODE 2) tuning of a variant: its own occupancy (no agreement test, no cycle jump), and
+// WPB > 1: workgroups of WPB waves -- every resident wave of a CU -- that take the listed sectors of a
+// contiguous share of the list from an LDS counter (bp_decode_kernel).
+template <class TU, int LW, int WPB = 0>
 struct ListTune : TU {
     static constexpr int kMinWavesSyn = LW;
+    static constexpr int kWavesPerBlock = WPB > 0 ? WPB : TU::kWavesPerBlock;
 };
 
 // the largest divisor of L not above the variant's column-group size
@@ -1566,7 +1569,32 @@ void bp_decode_kernel(const BpArgs a)
         const long long nw = (long long)gridDim.x * (blockDim.x >> 6);
         // (the next sectors' list entries and syndrome bits loaded ahead: no gain at p = 2e-3 / 5e-3, -3 %
         // at 1e-2; round 4)
-        for (long long vw = wave; vw < wTot; vw += nw) {
+        // With WPB > 1 (ListTune) a workgroup holds every wave of its CU, and they take the sectors of the
+        // workgroup's contiguous share one at a time from an LDS counter.  A SIMD issues its oldest wave first,
+        // so with a static share per wave the first-launched waves finish their sectors early and the launch
+        // ends on the youngest, nearly alone on their SIMDs (P61 at p = 5e-3: busy cycles per wave 0.61 M in
+        // the first quarter of the grid, 0.93 M in the last, max / mean 1.7; tools/kbench/list_phases.py):
+        // the counter lets a CU's waves finish together.
+        constexpr bool kQueue = waves_per_block<TU>() > 1;
+        __shared__ uint32_t next;
+        long long lo = wave, hi = wTot;
+        if constexpr (kQueue) {
+            if (threadIdx.x == 0) next = 0u;
+            __syncthreads();
+            const long long per = (wTot + gridDim.x - 1) / gridDim.x;
+            lo = (long long)blockIdx.x * per;
+            hi = lo + per < wTot ? lo + per : wTot;
+        }
+        for (long long t = 0;; ++t) {
+            long long vw;
+            if constexpr (kQueue) {
+                uint32_t k = 0u;
+                if (lane == 0) k = __hip_atomic_fetch_add(&next, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                vw = lo + (long long)__builtin_amdgcn_readfirstlane(k);
+            } else {
+                vw = lo + t * nw;  // a static grid stride
+            }
+            if (vw >= hi) break;
             const bool doX = vw < wXn;  // wave-uniform
             const long long slot = (doX ? vw : vw - wXn) * G + g;
             const bool in_range = (g < G) && (slot < (doX ? nX : nZ));
@@ -1617,7 +1645,10 @@ struct TuneP7MinReg : TuneP7 {};
 using ShiftsP7 = GeneratedShifts<3, 3, 6, 7, 2, 3, TuneP7::kRelabel, TuneP7::kMaskSelect>;
 // List mode (MODE 2): P61 at four waves per SIMD (<= 128 VGPRs; three: -5 % at p = 5e-3, -10 % at 1e-2;
 // five spill and lose 20-25 %, profiles/r05/, profiles/r06/ab/), P7 at five.
-using ListTuneP61 = ListTune<TuneP61, 4>;
+// ... in 16-wave workgroups, one per CU, that take their sectors from an LDS counter (bp_decode_kernel):
+// config 5 +12 % at p = 0.01, +6 % at 5e-3, +1 % at 2e-3 over a static grid stride
+// (profiles/r06/ab/cmp_list_cu.txt)
+using ListTuneP61 = ListTune<TuneP61, 4, 16>;
 using ListTuneP7 = ListTune<TuneP7MinReg, 5>;
 KernelFn p61_minreg_kernel(int stop, bool split);  // bp_decode_p61.hip
 KernelFn p61_minreg_seq_kernel(int stop, int sec); // bp_decode_p61.hip
@@ -1687,6 +1718,7 @@ struct Variant {
     const char* name;
     KernelFn list = nullptr;  // syndrome stop, list mode (MODE 2: the sectors the triage passed on)
     int min_waves_syn = 1;    // its occupancy (waves per SIMD), for the list launch's grid
+    int list_wpb = 1;         // its waves per workgroup
     KernelFn seq[3][2] = {};     // sector launches (MODE 3 / 4): [stop][sector]
     // QEC_OPT_SECTOR_SPLIT = 1 takes the sector launches from this batch on, per stop rule (0: never), and
     // under the syndrome stop only from seq_syn_min_p on
@@ -1732,6 +1764,7 @@ static Variant make_variant(int P, int S, int T, const char* name)
         v.seq[QEC_STOP_SYNDROME][1] = bp_decode_kernel<J, K, L, QEC_STOP_SYNDROME, SH, SeqSynTune<TU>, 4>;
     }
     v.min_waves_syn = TUL::kMinWavesSyn;  // the list launch's grid (launch_decode_list)
+    v.list_wpb = waves_per_block<TUL>();
     return v;
 }
 // Tune<min waves per SIMD, relabel, zero-skip, short division, hard-message paths, sector split,
@@ -1799,6 +1832,7 @@ static Variant gen_p7()
     v.split[QEC_STOP_SYNDROME] = p7_minreg_kernel(QEC_STOP_SYNDROME, true);
     v.list = p7_minreg_list_kernel();
     v.min_waves_syn = ListTuneP7::kMinWavesSyn;
+    v.list_wpb = waves_per_block<ListTuneP7>();
     return v;
 }
 
@@ -2036,9 +2070,9 @@ int launch_decode_list(const void* variant, const Code& c, const uint8_t* sX, co
     relabel(c.EZ.data(), c.K, c.L, c.P, v->relabel, a.SZ, a.DZ, a.CZ);
     // one wave per resident slot of the chip (more rounds of the grid measured no gain,
     // profiles/r03/list_rounds/), each looping over the listed sectors
-    const int wpb = v->waves_per_block;
+    const int wpb = v->list_wpb;
     const long long need = (2 * B + a.G - 1) / a.G;
-    const long long cap = 4LL * device_cus() * v->min_waves_syn;
+    const long long cap = 4LL * device_cus() * v->min_waves_syn;  // a multiple of wpb for the per-CU workgroups
     const long long waves = need < cap ? need : cap;
     const long long blocks = (waves + wpb - 1) / wpb;
     hipLaunchKernelGGL(v->list, dim3((unsigned)blocks), dim3(64 * wpb), 0, stream, a);

@@ -153,6 +153,9 @@ def main():
     ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
                     help="decoder option for the timed run (qec_decoder_set_option), e.g. schedule=0")
     ap.add_argument("--no-gather", action="store_true", help="N > 1: skip the RCCL gather measurements")
+    ap.add_argument("--gather-world1", action="store_true",
+                    help="N = 1: measure the gather paths in an RCCL group of one (the gather is rank 0's own copy; "
+                         "DESIGN.md section 9's world-1 rate)")
     ap.add_argument("--graph", action="store_true",
                     help="time the step as a replay of one captured HIP graph of it (same kernels, no per-launch "
                          "host work or inter-launch gaps); without it the replay is reported in `graph`")
@@ -362,12 +365,18 @@ def main():
     if args.graph:
         out["config"]["launch"] = "hip graph replay"
 
-    if world > 1 and not args.no_gather and packed:
+    solo = world == 1 and args.gather_world1 and packed
+    if solo:  # an RCCL group of one, after every timed measurement above
+        dist.init_process_group("nccl", init_method="tcp://127.0.0.1:%d" % free_port(), rank=0, world_size=1)
+        backend = "nccl"
+    if (world > 1 or solo) and not args.no_gather and packed:
         try:
             out["gather"] = gather_measure(dec, step, rec, B, world, rank, dev, stream, steps, global_batch, backend,
                                            bound_into)
         except Exception as exc:  # noqa: BLE001 -- a failure here must not cost the bench line
             out["gather"] = {"error": "%s: %s" % (type(exc).__name__, exc)}
+    if solo:
+        dist.destroy_process_group()
 
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(code, fname, sX, sZ, p, iters, args, outs, packed)
@@ -422,16 +431,19 @@ def graph_retime(step, S, dev, stream, B, outs, world, per_step_units, steps):
             "kernel_ms": round(kernel_ms, 4), "identical": bool(same)}
 
 
+def free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
 def relaunch(nproc):
     """Runs this script under `python -m torch.distributed.run --nproc-per-node nproc` (rendezvous on
     127.0.0.1) as a child process with the same arguments; returns its exit status."""
-    import socket
     import subprocess
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        port = s.getsockname()[1]
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
-           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.abspath(__file__)] + sys.argv[1:]
     return subprocess.run(cmd).returncode
 
 

@@ -85,3 +85,18 @@ def test_rccl_gather_and_counter_reduce_world1():
     assert out["pipeline_equal"] and out["pipeline_device"] == "cuda:0"
     assert out["counters_equal"] and out["tested"] == 8192
     assert out["times"] == [0.5, 0.25, 0.1, 0.9, 0.0]
+
+
+def test_bench_gather_world1():
+    """bench.py --gather-world1: the gather measurements (alone, serialised, overlapped) in an RCCL group of
+    one, the source of DESIGN.md section 9's world-1 rate; both record checks hold."""
+    r = subprocess.run([sys.executable, "bench.py", "--gather-world1", "--no-extras", "--no-cpu",
+                        "--global-batch", "65536", "--steps", "5"], cwd=ROOT, capture_output=True, text=True,
+                       timeout=240)
+    assert r.returncode == 0, "rc=%d\n%s\n%s" % (r.returncode, r.stdout[-3000:], r.stderr[-3000:])
+    out = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    g = out["gather"]
+    assert "error" not in g, g
+    assert g["backend"] == "nccl" and g["world_size"] == 1 and g["bytes_per_rank"] == 65536 * 155
+    assert g["rank0_shard_intact"] and g["end_to_end_overlapped"]["rank0_last_step_intact"]
+    assert g["gather_ms"] > 0 and g["end_to_end_overlapped"]["ms_per_step"] > 0

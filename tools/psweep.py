@@ -61,8 +61,10 @@ def mc_roofline(p, samples, stop, iters, batch, code_name):
     dom = pm["dominant"]
     k = pm["kernels"][dom]
     lds = k.get("lds_issue_frac") or 0.0
-    return {"dominant_kernel": dom, "bound": "lds" if lds > k.get("valu_issue_frac", 0.0) else "valu",
-            "frac": k.get("valu_issue_frac"), "lds_issue_frac": k.get("lds_issue_frac"),
+    valu = k.get("valu_issue_frac") or 0.0
+    return {"dominant_kernel": dom, "bound": "lds" if lds > valu else "valu",
+            "frac": max(lds, valu),  # the bound's issue fraction
+            "valu_issue_frac": k.get("valu_issue_frac"), "lds_issue_frac": k.get("lds_issue_frac"),
             "wait_over_issue": k.get("wait_over_issue"),
             "kernels_us": {n: round(v["avg_ns"] / 1e3, 1) for n, v in pm["kernels"].items()},
             "basis": "profiled dispatch times: SQ_INSTS_VALU x 2 / (1024 SIMDs x 2.4 GHz x time); LDS: SQ_INSTS_LDS "

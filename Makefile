@@ -8,7 +8,7 @@ CSRC     := qec_ldpc_amd/csrc
 OBJ      := build/obj
 LIB      := qec_ldpc_amd/libqecldpc.so
 OBJS     := $(OBJ)/bp_decode.o $(OBJ)/bp_decode_p61.o $(OBJ)/bp_decode_phase.o $(OBJ)/bp_sparse.o $(OBJ)/schedule.o $(OBJ)/triage.o $(OBJ)/montecarlo.o $(OBJ)/code_model.o $(OBJ)/cpu_engine.o $(OBJ)/capi.o
-HDRS     := include/qec_ldpc.h include/HostDeviceArray.h $(CSRC)/qec_internal.h $(CSRC)/qec_device.h $(CSRC)/qec_mc.h
+HDRS     := include/qec_ldpc.h include/HostDeviceArray.h $(CSRC)/qec_internal.h $(CSRC)/qec_device.h $(CSRC)/qec_mc.h $(CSRC)/qec_launch.h
 # build id: hash of every library source and this Makefile (identical for every rebuild of one tree);
 # profiles/pmc_*.json carry it and bench.py uses a profile only with the library it was taken on
 SRCS     := $(sort $(wildcard $(CSRC)/*.hip $(CSRC)/*.cpp $(CSRC)/*.h)) include/qec_ldpc.h include/HostDeviceArray.h Makefile

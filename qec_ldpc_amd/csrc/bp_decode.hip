@@ -39,6 +39,7 @@
 
 #include "qec_device.h"
 #include "qec_internal.h"
+#include "qec_launch.h"
 
 #pragma clang fp contract(off)
 
@@ -1931,7 +1932,8 @@ bool decode_has_phase_stats(const void* variant, int stop)
 int launch_decode(const void* variant, const Code& c, const uint8_t* sX, const uint8_t* sZ, bool sbits, long long B,
                   float errorProbability, int maxIter, int stop, uint8_t* eX, uint8_t* eZ, uint8_t* flags,
                   uint8_t* rec, int32_t* iters, float* q, int hardPaths, const int32_t* perm, int split,
-                  uint32_t* merge, bool merge_zeroed, hipStream_t stream, int rec_stride, bool perm_sectors)
+                  uint32_t* merge, bool merge_zeroed, hipStream_t stream, int rec_stride, bool perm_sectors,
+                  hipEvent_t done)
 {
     const Variant* v = static_cast<const Variant*>(variant);
     if (B <= 0) return QEC_OK;
@@ -1979,14 +1981,15 @@ int launch_decode(const void* variant, const Code& c, const uint8_t* sX, const u
         if (merge == nullptr) return fail(QEC_ERR_ARG, "bp_decode: sector launches need the merge words");
         a.merge = merge;
         for (int sec = 0; sec < 2; ++sec) {
-            hipLaunchKernelGGL(v->seq[stop][sec], dim3((unsigned)blocks), dim3(64 * wavesPerBlock), 0, stream, a);
+            launch_marked(v->seq[stop][sec], dim3((unsigned)blocks), dim3(64 * wavesPerBlock), 0, stream, nullptr,
+                          sec == 1 ? done : nullptr, a);
             hipError_t err = hipGetLastError();
             if (err != hipSuccess) return fail(QEC_ERR_HIP, std::string("bp_decode launch: ") + hipGetErrorString(err));
         }
         return QEC_OK;
     }
-    hipLaunchKernelGGL(phase ? v->phase[stop] : split ? v->split[stop] : v->fn[stop], dim3((unsigned)blocks),
-                       dim3(64 * wavesPerBlock), 0, stream, a);
+    launch_marked(phase ? v->phase[stop] : split ? v->split[stop] : v->fn[stop], dim3((unsigned)blocks),
+                  dim3(64 * wavesPerBlock), 0, stream, nullptr, done, a);
     hipError_t err = hipGetLastError();
     if (err != hipSuccess) return fail(QEC_ERR_HIP, std::string("bp_decode launch: ") + hipGetErrorString(err));
     return QEC_OK;
@@ -2045,7 +2048,7 @@ bool decode_pattern_masks(const void* variant, float errorProbability, uint32_t 
 int launch_decode_list(const void* variant, const Code& c, const uint8_t* sX, const uint8_t* sZ, long long B,
                        float errorProbability, int maxIter, int hardPaths, uint8_t* rec, int32_t* iters,
                        uint32_t* merge, const int32_t* listX, const int32_t* listZ, const uint32_t* counts,
-                       hipStream_t stream, int rec_stride, bool merge_only, int count_stride)
+                       hipStream_t stream, int rec_stride, bool merge_only, int count_stride, hipEvent_t done)
 {
     const Variant* v = static_cast<const Variant*>(variant);
     if (!v->list) return fail(QEC_ERR_UNSUPPORTED, "bp_decode: no list-mode kernel for this code");
@@ -2075,7 +2078,7 @@ int launch_decode_list(const void* variant, const Code& c, const uint8_t* sX, co
     const long long cap = 4LL * device_cus() * v->min_waves_syn;  // a multiple of wpb for the per-CU workgroups
     const long long waves = need < cap ? need : cap;
     const long long blocks = (waves + wpb - 1) / wpb;
-    hipLaunchKernelGGL(v->list, dim3((unsigned)blocks), dim3(64 * wpb), 0, stream, a);
+    launch_marked(v->list, dim3((unsigned)blocks), dim3(64 * wpb), 0, stream, nullptr, done, a);
     const hipError_t err = hipGetLastError();
     if (err != hipSuccess) return fail(QEC_ERR_HIP, std::string("bp_decode list launch: ") + hipGetErrorString(err));
     return QEC_OK;

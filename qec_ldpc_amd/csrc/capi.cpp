@@ -12,13 +12,21 @@
 #include "../../include/HostDeviceArray.h"
 #include "qec_internal.h"
 
+namespace {
+// The handle's own events order work on one device (the workspace's cross-stream event) or time it
+// (the Monte-Carlo ring); neither needs the system-scope release of a default event record (a cache
+// writeback and invalidation between the launches around it; profiles/r06/ab/cmp_event_fence.txt).
+constexpr unsigned kEvNoFence = hipEventDisableSystemFence;
+}  // namespace
+
 namespace qec {
 const char* last_error_cstr();
 const void* select_variant(const Code& c, std::string& name);
 int launch_decode(const void* variant, const Code& c, const uint8_t* sX, const uint8_t* sZ, bool sbits, long long B,
                   float errorProbability, int maxIter, int stop, uint8_t* eX, uint8_t* eZ, uint8_t* flags,
                   uint8_t* rec, int32_t* iters, float* q, int hardPaths, const int32_t* perm, int split,
-                  uint32_t* merge, bool merge_zeroed, hipStream_t stream, int rec_stride = 0, bool perm_sectors = false);
+                  uint32_t* merge, bool merge_zeroed, hipStream_t stream, int rec_stride = 0, bool perm_sectors = false,
+                  hipEvent_t done = nullptr);
 size_t schedule_workspace_bytes(long long B, int mX, int mZ);
 bool schedule_sector_order(long long B, bool sbits, int mX, int mZ);
 long long schedule_max_batch();
@@ -33,7 +41,7 @@ bool decode_pattern_masks(const void* variant, float errorProbability, uint32_t 
 int launch_decode_list(const void* variant, const Code& c, const uint8_t* sX, const uint8_t* sZ, long long B,
                        float errorProbability, int maxIter, int hardPaths, uint8_t* rec, int32_t* iters,
                        uint32_t* merge, const int32_t* listX, const int32_t* listZ, const uint32_t* counts,
-                       hipStream_t stream, int rec_stride, bool merge_only, int count_stride);
+                       hipStream_t stream, int rec_stride, bool merge_only, int count_stride, hipEvent_t done = nullptr);
 bool triage_supported(const Code& c);
 bool triage_aligned(const void* sX, const void* sZ);
 int launch_triage(const Code& c, const uint32_t* sX, const uint32_t* sZ, long long B, const uint32_t pats[4],
@@ -216,10 +224,13 @@ int ws_acquire(qec_decoder* d, hipStream_t st)
     if (d->ws_used && st != d->ws_stream && !capturing(st)) QEC_HIP_CHECK(hipStreamWaitEvent(st, d->ws_ev, 0));
     return QEC_OK;
 }
-int ws_release(qec_decoder* d, hipStream_t st)
+// The workspace event for the call's last kernel to carry (launch_marked), or null while capturing;
+// ws_release(d, st, true) then records nothing more.
+hipEvent_t ws_done(qec_decoder* d, hipStream_t st) { return capturing(st) ? nullptr : d->ws_ev; }
+int ws_release(qec_decoder* d, hipStream_t st, bool carried = false)
 {
     if (capturing(st)) return QEC_OK;
-    QEC_HIP_CHECK(hipEventRecord(d->ws_ev, st));
+    if (!carried) QEC_HIP_CHECK(hipEventRecord(d->ws_ev, st));
     d->ws_used = true;
     d->ws_stream = st;
     return QEC_OK;
@@ -375,7 +386,7 @@ qec_decoder* qec_decoder_create_engine(const qec_code* h, int device, size_t max
         d->variant_name = sparse_plan_name(d->sparse);
     }
     if (hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&d->ws_ev, hipEventDisableTiming) != hipSuccess) {
+        hipEventCreateWithFlags(&d->ws_ev, hipEventDisableTiming | kEvNoFence) != hipSuccess) {
         fail(QEC_ERR_HIP, "qec_decoder_create: stream / event creation failed");
         return nullptr;
     }
@@ -612,10 +623,10 @@ int dispatch_decode(qec_decoder* d, const uint8_t* sX, const uint8_t* sZ, long l
                            iters, d->merge.data(), lX, lZ, cnt, st, rec_stride);
         if (!rc)
             rc = launch_decode_list(d->variant, c, sX, sZ, B, p, maxIter, hp, rec, iters, d->merge.data(), lX, lZ, cnt, st,
-                                    rec_stride, false, 1);
+                                    rec_stride, false, 1, ws_done(d, st));
         if (rc) return rc;
         d->last_path |= QEC_PATH_TRIAGE;
-        return ws_release(d, st);
+        return ws_release(d, st, true);
     }
     // QEC_OPT_SECTOR_SPLIT = 1 resolved per launch (the variant's measured choice for this stop, batch and p)
     int split_opt = decode_sector_mode(d->variant, stop, d->sector_split, B, p);
@@ -654,11 +665,12 @@ int dispatch_decode(qec_decoder* d, const uint8_t* sX, const uint8_t* sZ, long l
         zeroed = split;
     }
     rc = launch_decode(d->variant, c, sX, sZ, sbits, B, p, maxIter, stop, eX, eZ, flags, rec, iters, q, hp, perm,
-                       split_opt, need_merge ? d->merge.data() : nullptr, zeroed, st, rec_stride, perm_sectors);
+                       split_opt, need_merge ? d->merge.data() : nullptr, zeroed, st, rec_stride, perm_sectors,
+                       ws_done(d, st));
     if (rc) return rc;
     d->last_path |= (perm ? QEC_PATH_ORDERED : 0) | (perm && perm_sectors ? QEC_PATH_SECTOR_ORDER : 0) |
                     (split ? QEC_PATH_SPLIT_WAVES : 0) | (need_merge && !split ? QEC_PATH_SECTOR_LAUNCHES : 0);
-    return ws_release(d, st);
+    return ws_release(d, st, true);
 }
 
 const int32_t* syndrome_table(const qec_decoder* d)
@@ -897,6 +909,8 @@ int mc_batch(qec_decoder* d, McArgsHost h, int src, float p, int maxIter, int st
             QEC_HIP_CHECK(hipMemsetAsync(d->mcount.data(), 0, (QEC_MC_NCOUNTERS_ALL + mc_count_u64()) * sizeof(unsigned long long), st));
         else
             QEC_HIP_CHECK(hipMemsetAsync(cnt, 0, mc_count_u64() * sizeof(unsigned long long), st));
+        // the events here are separate records: carried by the kernels (launch_marked) this pipeline ran
+        // 1.5-2.4 % slower at p = 0.001 .. 0.005 (profiles/r06/ab/cmp_event_carry.txt)
         if (ev0) QEC_HIP_CHECK(hipEventRecord(ev0, st));
         auto fused = [&](int stage) {
             return launch_mc_fused(c, h.seed, h.start, B, h.p, pats, sXp, sZp, d->mrec.data(), rstride, d->mit.data(),
@@ -970,7 +984,7 @@ int monte_carlo_part(qec_decoder* d, uint64_t seed, uint64_t start, uint64_t cou
     // decode-kernel time from a ring of event pairs: the host waits only on a pair it reuses,
     // kRing batches behind the launches (no per-batch synchronisation)
     constexpr size_t kRing = 32;
-    if (d->mc_ev.ev.empty() && (rc = d->mc_ev.make(2 * kRing, hipEventDefault))) return rc;  // once per handle
+    if (d->mc_ev.ev.empty() && (rc = d->mc_ev.make(2 * kRing, hipEventDefault | kEvNoFence))) return rc;  // once per handle
     EventSet& ev = d->mc_ev;
     double dec = 0;
     uint64_t k = 0;

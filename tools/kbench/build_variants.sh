@@ -1,7 +1,7 @@
 #!/bin/bash
 # Build experimental variants of libqecldpc.so into build/variants/<name>/ (same sources,
-# different compile flags / macros for bp_decode.hip, triage.hip and schedule.hip; the other objects
-# are shared).
+# different compile flags / macros for bp_decode.hip, triage.hip, schedule.hip and capi.cpp; the other
+# objects are shared).
 # Used by tools/kbench/compare.py on the GPU box.
 #   tools/kbench/build_variants.sh name[:flags] ...     e.g.  cur  pipe:-DQEC_PIPELINE=1
 # SRCDIR=dir builds the variants from dir/bp_decode*.hip instead (e.g. an older revision for an A/B;
@@ -19,7 +19,6 @@ common() {
 common qec_ldpc_amd/csrc/code_model.cpp -x c++ &
 common qec_ldpc_amd/csrc/cpu_engine.cpp -x c++ &
 common qec_ldpc_amd/csrc/montecarlo.hip &
-common qec_ldpc_amd/csrc/capi.cpp -x hip &
 common qec_ldpc_amd/csrc/bp_sparse.hip &
 wait
 SRC=${SRCDIR:-qec_ldpc_amd/csrc}
@@ -33,8 +32,9 @@ build() {
   $HIPCC $BASE -DQEC_KBENCH_MINIMAL -I qec_ldpc_amd/csrc "$@" -c $SRC/bp_decode_phase.hip -o $out/bp_decode_phase.o
   $HIPCC $BASE -I qec_ldpc_amd/csrc "$@" -c qec_ldpc_amd/csrc/triage.hip -o $out/triage.o
   $HIPCC $BASE -I qec_ldpc_amd/csrc "$@" -c qec_ldpc_amd/csrc/schedule.hip -o $out/schedule.o
+  $HIPCC $BASE -I qec_ldpc_amd/csrc -x hip "$@" -c qec_ldpc_amd/csrc/capi.cpp -o $out/capi.o
   $HIPCC --offload-arch=gfx950 -shared -fPIC -o $out/libqecldpc.so $out/bp_decode.o $out/bp_decode_p61.o \
-      $out/bp_decode_phase.o $out/triage.o $out/schedule.o $COMMON/*.o
+      $out/bp_decode_phase.o $out/triage.o $out/schedule.o $out/capi.o $(ls $COMMON/*.o | grep -v /capi.o)
   echo "built $name"
 }
 pids=()

@@ -201,9 +201,13 @@ int qec_decoder_device(const qec_decoder* dec);         /* HIP device ordinal (o
  *     with a sector that goes on reach HBM (list-mode decode, then their statistics).
  *   QEC_OPT_LAST_PATH (read only; qec_decoder_set_option refuses it): the launch sequence the
  *     handle's last decode call enqueued, as QEC_PATH_* bits (0 before the first decode), so a test
- *     can assert which kernels its comparison went through. */
+ *     can assert which kernels its comparison went through.
+ *   QEC_OPT_MC_DECODE_TIME (default 1): qec_monte_carlo times its decode kernels with an event pair
+ *     per batch (qec_mc_result.decodeSeconds).  0: no events between its launches (each costs the
+ *     GPU a few microseconds, ~5 % of a 2^20-sample batch at p = 0.001) and decodeSeconds = 0;
+ *     counters unchanged. */
 enum { QEC_OPT_HARD_PATHS = 1, QEC_OPT_CYCLE_JUMP = 2, QEC_OPT_SCHEDULE = 3, QEC_OPT_SECTOR_SPLIT = 4,
-       QEC_OPT_PHASE_STATS = 5, QEC_OPT_TRIAGE = 6, QEC_OPT_LAST_PATH = 7 };
+       QEC_OPT_PHASE_STATS = 5, QEC_OPT_TRIAGE = 6, QEC_OPT_LAST_PATH = 7, QEC_OPT_MC_DECODE_TIME = 8 };
 enum {
     QEC_PATH_ORDERED = 1,          /* dispatch order pass (schedule.hip) */
     QEC_PATH_SECTOR_ORDER = 2,     /* ... in the per-sector form (each sector's waves by its own weight) */

@@ -27,7 +27,7 @@ CONVERGENCE_FAIL_Z = 8
 STOP = {"ref": 0, "fixed": 1, "syndrome": 2}
 ENGINE = {"auto": 0, "circulant": 1, "sparse": 2, "cpu": 3}
 OPTION = {"hard_paths": 1, "cycle_jump": 2, "schedule": 3, "sector_split": 4, "phase_stats": 5, "triage": 6,
-          "last_path": 7}
+          "last_path": 7, "mc_decode_time": 8}
 # QEC_PATH_* bits of QEC_OPT_LAST_PATH (include/qec_ldpc.h): the launch sequence of the last decode call
 PATH = {"ordered": 1, "sector_order": 2, "split_waves": 4, "sector_launches": 8, "triage": 16, "bit_rows": 32,
         "sparse": 64, "records": 128}

@@ -58,6 +58,7 @@ int launch_mc_fused(const Code& c, uint64_t seed, uint64_t start, long long B, f
                     int32_t* listX, int32_t* listZ, int32_t* listS, uint32_t* counts, const uint64_t* imp_cols,
                     unsigned long long* counters, unsigned long long* partials, int stage, hipStream_t st);
 long long mc_fused_parts(long long B);
+int launch_zero_words(unsigned long long* w, int n, hipStream_t st);
 int mc_fused_count_words();
 int mc_fused_count_stride();
 // u64 words after the counters that hold the fused pipeline's list lengths
@@ -124,6 +125,7 @@ struct qec_decoder {
     int phase_stats = 0;            // QEC_OPT_PHASE_STATS
     int triage = 1;                 // QEC_OPT_TRIAGE
     int last_path = 0;              // QEC_OPT_LAST_PATH: QEC_PATH_* bits of the last decode call
+    int mc_time = 1;                // QEC_OPT_MC_DECODE_TIME
     // workspace shared by every launch of this handle (dispatch order, split-flag merge words,
     // sparse byte staging for packed output); ws_ev marks the last launch that used it, so a call
     // on another stream waits for it (stream-ordered reuse)
@@ -515,6 +517,7 @@ int qec_decoder_set_option(qec_decoder* d, int option, int value)
         if (value < 0 || value > 3) return fail(QEC_ERR_ARG, "qec_decoder_set_option: QEC_OPT_TRIAGE is 0 .. 3");
         d->triage = value;
         return QEC_OK;
+    case QEC_OPT_MC_DECODE_TIME: d->mc_time = value != 0; return QEC_OK;
     case QEC_OPT_LAST_PATH: return fail(QEC_ERR_ARG, "qec_decoder_set_option: QEC_OPT_LAST_PATH is read only");
     default: return fail(QEC_ERR_ARG, "qec_decoder_set_option: unknown option");
     }
@@ -531,6 +534,7 @@ int qec_decoder_get_option(const qec_decoder* d, int option, int* value)
     case QEC_OPT_PHASE_STATS: *value = d->phase_stats; return QEC_OK;
     case QEC_OPT_TRIAGE: *value = d->triage; return QEC_OK;
     case QEC_OPT_LAST_PATH: *value = d->parts.empty() ? d->last_path : d->parts[0]->last_path; return QEC_OK;
+    case QEC_OPT_MC_DECODE_TIME: *value = d->mc_time; return QEC_OK;
     default: return fail(QEC_ERR_ARG, "qec_decoder_get_option: unknown option");
     }
 }
@@ -905,10 +909,9 @@ int mc_batch(qec_decoder* d, McArgsHost h, int src, float p, int maxIter, int st
         uint32_t* cnt = reinterpret_cast<uint32_t*>(d->mcount.data() + QEC_MC_NCOUNTERS_ALL);  // list lengths
         uint32_t* sXp = reinterpret_cast<uint32_t*>(d->msX.data());
         uint32_t* sZp = reinterpret_cast<uint32_t*>(d->msZ.data());
-        if (zero_counters)
-            QEC_HIP_CHECK(hipMemsetAsync(d->mcount.data(), 0, (QEC_MC_NCOUNTERS_ALL + mc_count_u64()) * sizeof(unsigned long long), st));
-        else
-            QEC_HIP_CHECK(hipMemsetAsync(cnt, 0, mc_count_u64() * sizeof(unsigned long long), st));
+        rc = zero_counters ? launch_zero_words(d->mcount.data(), QEC_MC_NCOUNTERS_ALL + mc_count_u64(), st)
+                           : launch_zero_words(d->mcount.data() + QEC_MC_NCOUNTERS_ALL, mc_count_u64(), st);
+        if (rc) return rc;
         // the events here are separate records: carried by the kernels (launch_marked) this pipeline ran
         // 1.5-2.4 % slower at p = 0.001 .. 0.005 (profiles/r06/ab/cmp_event_carry.txt)
         if (ev0) QEC_HIP_CHECK(hipEventRecord(ev0, st));
@@ -997,11 +1000,12 @@ int monte_carlo_part(qec_decoder* d, uint64_t seed, uint64_t start, uint64_t cou
     };
     for (uint64_t base = 0; base < count; base += batch, ++k) {
         const size_t slot = k % kRing;
-        if (k >= kRing && (rc = harvest(slot))) return rc;
+        if (d->mc_time && k >= kRing && (rc = harvest(slot))) return rc;
         McArgsHost h;
         h.seed = seed; h.start = start + base; h.p = p;
         h.B = (long long)std::min<uint64_t>(batch, count - base);
-        rc = mc_batch(d, h, MC_SRC_PHILOX, p, maxIter, stop, true, ev.ev[2 * slot], ev.ev[2 * slot + 1], k == 0);
+        rc = mc_batch(d, h, MC_SRC_PHILOX, p, maxIter, stop, true, d->mc_time ? ev.ev[2 * slot] : nullptr,
+                      d->mc_time ? ev.ev[2 * slot + 1] : nullptr, k == 0);
         if (rc) return rc;
     }
     if (k == 0)  // no batch zeroed the counters
@@ -1010,7 +1014,7 @@ int monte_carlo_part(qec_decoder* d, uint64_t seed, uint64_t start, uint64_t cou
     // event pairs are complete by then (qec_monte_carlo reads the counters from mhost)
     if ((rc = mc_enqueue_counters(d))) return rc;
     QEC_HIP_CHECK(hipStreamSynchronize(st));
-    for (uint64_t j = k > kRing ? k - kRing : 0; j < k; ++j)
+    for (uint64_t j = k > kRing ? k - kRing : 0; d->mc_time && j < k; ++j)
         if ((rc = harvest(j % kRing))) return rc;
     *decode_s = dec;
     return QEC_OK;

@@ -652,12 +652,15 @@ __global__ __launch_bounds__(64 * kFusedWaves, kFusedMinWaves) void mc_fused_ker
         wgbase[threadIdx.x] = tot ? atomicAdd(&a.counts[threadIdx.x * kCountStride], tot) : 0u;
     }
     __syncthreads();
-    uint32_t base[3] = {wgbase[0], wgbase[1], wgbase[2]};
-    for (int w = 0; w < wv; ++w)
-        for (int k = 0; k < 3; ++k) base[k] += wcnt[w][k];
-    if ((gx >> lane) & 1ull) a.listX[base[0] + __popcll(gx & lt)] = (int32_t)b;
-    if ((gz >> lane) & 1ull) a.listZ[base[1] + __popcll(gz & lt)] = (int32_t)b;
-    if ((gs >> lane) & 1ull) a.listS[base[2] + __popcll(gs & lt)] = (int32_t)b;
+    uint32_t bX = wgbase[0], bZ = wgbase[1], bS = wgbase[2];
+    for (int w = 0; w < wv; ++w) {
+        bX += wcnt[w][0];
+        bZ += wcnt[w][1];
+        bS += wcnt[w][2];
+    }
+    if ((gx >> lane) & 1ull) a.listX[bX + __popcll(gx & lt)] = (int32_t)b;
+    if ((gz >> lane) & 1ull) a.listZ[bZ + __popcll(gz & lt)] = (int32_t)b;
+    if ((gs >> lane) & 1ull) a.listS[bS + __popcll(gs & lt)] = (int32_t)b;
     store_partials<kFusedWaves>(c, part, a.partials);
 }
 
@@ -747,6 +750,17 @@ __global__ __launch_bounds__(64 * kSurvWaves) void mc_survivor_kernel(const Fuse
         const long long idx = i0 + lane;
         const bool valid = idx < cnt;
         const long long b = valid ? a.listS[idx] : 0;
+        // the sample's record words, merge word and iteration counts are loaded before the walk, so
+        // their latency overlaps it (the kernel is latency-bound: few survivors per CU)
+        const uint32_t* __restrict__ r = reinterpret_cast<const uint32_t*>(a.rec + b * a.recB);
+        constexpr int kRW = (2 * nb + 3) / 4;  // record words holding decisions
+        static_assert(kRW <= 2 * NW, "the lane region holds the record's words");
+        uint32_t rw[kRW];
+#pragma unroll
+        for (int d = 0; d < kRW; ++d) rw[d] = valid ? r[d] : 0u;
+        const uint32_t mw = valid ? a.merge[b] : 0u;
+        int2 it2 = make_int2(0, 0);
+        if (valid) it2 = *reinterpret_cast<const int2*>(a.iters + 2 * b);
         for (int k = 0; k < RS; ++k) mine[k] = 0u;
         if (valid && a.gp.thr != 0) {
             gap_walk(a.gp, a.start + (uint64_t)b, n, T, [&](int v, uint32_t t) {
@@ -755,17 +769,13 @@ __global__ __launch_bounds__(64 * kSurvWaves) void mc_survivor_kernel(const Fuse
             });
         }
         // residual = errors ^ decisions over the record's 2 nb decision bytes
-        const uint32_t* __restrict__ r = reinterpret_cast<const uint32_t*>(a.rec + b * a.recB);
-        constexpr int kRW = (2 * nb + 3) / 4;  // record words holding decisions
-        static_assert(kRW <= 2 * NW, "the lane region holds the record's words");
-        const uint32_t mw = valid ? a.merge[b] : 0u;
         const bool xclean = (mw & kXClean) != 0u;  // X residual 0; no X record words
         uint32_t nz = 0;
         uint64_t nzw = 0;  // nonzero residual words
         static_assert(kRW <= 64, "one mask bit per residual word");
 #pragma unroll
         for (int d = 0; d < kRW; ++d) {
-            const uint32_t rv = valid ? r[d] : 0u;
+            const uint32_t rv = rw[d];
             const int rem = 2 * nb - 4 * d;  // decision bytes in word d
             const int xb = n - 32 * d;       // X decision bits in word d
             const uint32_t xm = xb >= 32 ? ~0u : xb <= 0 ? 0u : (1u << xb) - 1u;
@@ -808,12 +818,7 @@ __global__ __launch_bounds__(64 * kSurvWaves) void mc_survivor_kernel(const Fuse
         c[C_CORRECTED] += __popcll(ok & ~logical);
         c[C_CONVX] += __popcll(__ballot((f & QEC_CONVERGENCE_FAIL_X) != 0));
         c[C_CONVZ] += __popcll(__ballot((f & QEC_CONVERGENCE_FAIL_Z) != 0));
-        unsigned long long itx = 0, itz = 0;
-        if (valid) {
-            const int2 it = *reinterpret_cast<const int2*>(a.iters + 2 * b);
-            itx = (unsigned)it.x;
-            itz = (unsigned)it.y;
-        }
+        unsigned long long itx = (unsigned)it2.x, itz = (unsigned)it2.y;
 #pragma unroll
         for (int o = 32; o >= 1; o >>= 1) {
             itx += __shfl_xor(itx, o);
@@ -936,6 +941,23 @@ int launch_mc_fused(const Code& c, uint64_t seed, uint64_t start, long long B, f
     }
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(QEC_ERR_HIP, std::string("mc fused launch: ") + hipGetErrorString(e));
+    return QEC_OK;
+}
+
+// Zeroes n 64-bit words on the stream (the fused pipeline's counters and list lengths before a batch):
+// a one-workgroup kernel of this library instead of hipMemsetAsync, whose fill launch left ~4 us of
+// idle GPU before the next kernel (profiles/r06/ab/cmp_zero_kernel.txt)
+__global__ __launch_bounds__(256) void zero_words_kernel(unsigned long long* __restrict__ w, int n)
+{
+    for (int i = threadIdx.x; i < n; i += blockDim.x) w[i] = 0ull;
+}
+
+int launch_zero_words(unsigned long long* w, int n, hipStream_t st)
+{
+    if (n <= 0) return QEC_OK;
+    hipLaunchKernelGGL(zero_words_kernel, dim3(1), dim3(256), 0, st, w, n);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(QEC_ERR_HIP, std::string("zero words launch: ") + hipGetErrorString(e));
     return QEC_OK;
 }
 

@@ -155,6 +155,24 @@ def test_monte_carlo_fused_batches_and_empty_run(env):
         assert empty[k] == 0, k
 
 
+def test_monte_carlo_without_decode_timing(env):
+    """QEC_OPT_MC_DECODE_TIME 0 (tools/psweep.py's timed runs): the same counters on the fused low-p
+    pipeline and the ordered one over several batches, decodeSeconds 0; back on, timed again."""
+    code, dec, _ = env["P61"]
+    for p, batch in ((0.002, 4096), (0.03, 2048)):
+        timed = dec.monte_carlo(13, 0, 9000, p, 50, "syndrome", batch=batch)
+        dec.set_option("mc_decode_time", 0)
+        try:
+            assert dec.get_option("mc_decode_time") == 0
+            bare = dec.monte_carlo(13, 0, 9000, p, 50, "syndrome", batch=batch)
+        finally:
+            dec.set_option("mc_decode_time", 1)
+        for k in q.MC_COUNTERS + ("tested", "iterationsX", "iterationsZ"):
+            assert bare[k] == timed[k], (p, k)
+        assert bare["decodeSeconds"] == 0.0 and timed["decodeSeconds"] > 0.0
+        assert dec.monte_carlo(13, 0, 9000, p, 50, "syndrome", batch=batch)["decodeSeconds"] > 0.0
+
+
 def test_monte_carlo_full_batch(env):
     """qec_monte_carlo at psweep's default shape (2^20 samples in one batch: 64-lane front-end waves,
     one decode launch) against oracle counting on its last 2 048 samples (the same launch shape minus

@@ -19,7 +19,8 @@ from qec_ldpc_amd.codes import P7, P61, code_path  # noqa: E402
 from qec_ldpc_amd.synthetic import depolarizing_errors  # noqa: E402
 
 CODES = {"p61": (P61, 0.01, 50), "p7": (P7, 0.02, 20)}
-OPTIONS = {"hard_paths": 1, "cycle_jump": 2, "schedule": 3, "sector_split": 4, "phase_stats": 5, "triage": 6}
+OPTIONS = {"hard_paths": 1, "cycle_jump": 2, "schedule": 3, "sector_split": 4, "phase_stats": 5, "triage": 6,
+           "mc_decode_time": 8}
 
 
 def bind(path):
@@ -79,6 +80,9 @@ def mc_main(a, name, p, iters):
         ms = float(np.median([x[0] for x in res[v]])) * 1e3
         dms = float(np.median([x[1] for x in res[v]])) * 1e3
         print("%-22s %9.3f ms  %12.0f syn/s  decode %.3f ms  identical=%s" % (v, ms, a.batch / ms * 1e3, dms, cnt[v] == ref))
+        print(json.dumps({"variant": v, "counters": dict(zip(("tested", "withX", "withZ", "synX", "synZ", "logical",
+                                                               "corrected", "convX", "convZ", "iterationsX",
+                                                               "iterationsZ"), cnt[v]))}))
 
 
 def main():

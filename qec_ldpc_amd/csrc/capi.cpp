@@ -58,7 +58,8 @@ int launch_mc_fused(const Code& c, uint64_t seed, uint64_t start, long long B, f
                     int32_t* listX, int32_t* listZ, int32_t* listS, uint32_t* counts, const uint64_t* imp_cols,
                     unsigned long long* counters, unsigned long long* partials, int stage, hipStream_t st);
 long long mc_fused_parts(long long B);
-int launch_zero_words(unsigned long long* w, int n, hipStream_t st);
+int launch_zero_words(unsigned long long* w, int n, hipStream_t st, unsigned long long* w2 = nullptr, int n2 = 0);
+int mc_fused_part_rows();
 int mc_fused_count_words();
 int mc_fused_count_stride();
 // u64 words after the counters that hold the fused pipeline's list lengths
@@ -146,7 +147,7 @@ struct qec_decoder {
     DeviceArray<uint8_t> msX, msZ, merrp, mrec, mtype;
     DeviceArray<int32_t> mit, midx;
     DeviceArray<unsigned long long> mcount;
-    DeviceArray<unsigned long long> mpart;  // fused Monte-Carlo kernel: per-workgroup counter sums
+    DeviceArray<unsigned long long> mpart;  // fused Monte-Carlo kernel: partial-sum rows of the counters
     PinnedArray<unsigned long long> mhost;  // the counters' host copy (page-locked: an asynchronous copy)
     EventSet mc_ev;  // qec_monte_carlo's ring of decode-time event pairs
     // multi-device group (qec_decoder_create_multi): the parts do the work, this handle only routes
@@ -901,7 +902,7 @@ int mc_batch(qec_decoder* d, McArgsHost h, int src, float p, int maxIter, int st
         if (rc) return rc;
         if ((rc = ws_reserve(d->merge, (size_t)B, st, "monte carlo")) ||
             (rc = ws_reserve(d->tlist, 3 * (size_t)B, st, "monte carlo")) ||
-            (rc = ws_reserve(d->mpart, (size_t)mc_fused_parts(B) * QEC_MC_NCOUNTERS_ALL, st, "monte carlo")))
+            (rc = ws_reserve(d->mpart, (size_t)mc_fused_part_rows() * QEC_MC_NCOUNTERS_ALL, st, "monte carlo")))
             return rc;
         int32_t* lX = d->tlist.data();
         int32_t* lZ = lX + B;
@@ -909,8 +910,10 @@ int mc_batch(qec_decoder* d, McArgsHost h, int src, float p, int maxIter, int st
         uint32_t* cnt = reinterpret_cast<uint32_t*>(d->mcount.data() + QEC_MC_NCOUNTERS_ALL);  // list lengths
         uint32_t* sXp = reinterpret_cast<uint32_t*>(d->msX.data());
         uint32_t* sZp = reinterpret_cast<uint32_t*>(d->msZ.data());
-        rc = zero_counters ? launch_zero_words(d->mcount.data(), QEC_MC_NCOUNTERS_ALL + mc_count_u64(), st)
-                           : launch_zero_words(d->mcount.data() + QEC_MC_NCOUNTERS_ALL, mc_count_u64(), st);
+        // the counters (first batch), the list lengths and the partial-sum rows, in one launch
+        const int nz = mc_fused_part_rows() * QEC_MC_NCOUNTERS_ALL;
+        rc = zero_counters ? launch_zero_words(d->mcount.data(), QEC_MC_NCOUNTERS_ALL + mc_count_u64(), st, d->mpart.data(), nz)
+                           : launch_zero_words(d->mcount.data() + QEC_MC_NCOUNTERS_ALL, mc_count_u64(), st, d->mpart.data(), nz);
         if (rc) return rc;
         // the events here are separate records: carried by the kernels (launch_marked) this pipeline ran
         // 1.5-2.4 % slower at p = 0.001 .. 0.005 (profiles/r06/ab/cmp_event_carry.txt)

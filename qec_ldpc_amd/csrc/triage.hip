@@ -386,8 +386,8 @@ __global__ __launch_bounds__(64 * kTriageWaves) void triage_kernel(const TriageA
 // 4-wave workgroups: six fit a CU's LDS (23 words per lane for P61: rows and up to six hits) and the
 // registers are held to six waves per SIMD (measured against 8, 12 and 16-wave workgroups and ten or
 // sixteen hits: +2-9 %; a sample with more hits is a survivor); the list appends take one atomic
-// per workgroup and list, and the counters go to per-workgroup partial sums that
-// mc_survivor_kernel's first workgroups add up (same-address atomics serialise at L2)
+// per workgroup and list, and the counters are added into 64 rows of partial sums (workgroup mod 64:
+// same-address atomics serialise at L2) that mc_survivor_kernel's workgroup 0 adds up
 #ifndef QEC_FUSED_WAVES
 #define QEC_FUSED_WAVES 4
 #endif
@@ -421,11 +421,17 @@ struct FusedArgs {
     const uint64_t* imp_cols;
     int imp_cw;
     unsigned long long* counters;  // [C_N + 2] (iteration sums at C_N, C_N + 1)
-    unsigned long long* partials;  // [fused grid][C_N + 2]: mc_fused_kernel's per-workgroup sums
+    unsigned long long* partials;  // [kPartRows][C_N + 2]: mc_fused_kernel's partial-sum rows (zeroed first)
     int nparts;                    // its grid size
 };
 
-// the workgroup's counters (each wave's ballot popcounts) stored as its row of partials
+// The fused kernel's workgroups add their counters into kPartRows rows of partial sums (row = workgroup
+// mod kPartRows: ~64 same-address atomics per counter instead of 4 096, zeroed with the list lengths before
+// the kernel); mc_survivor_kernel's workgroup 0 adds the rows into the counters.
+constexpr int kPartRows = 64;
+static_assert(C_N + 2 == QEC_MC_NCOUNTERS_ALL, "a partial-sum row is the counter vector");
+
+// the workgroup's counters (each wave's ballot popcounts) added into its row of partials
 template <int NWAVES>
 __device__ __forceinline__ void store_partials(const unsigned long long (&c)[C_N + 2], unsigned long long (*part)[C_N + 2],
                                                unsigned long long* __restrict__ partials)
@@ -441,7 +447,7 @@ __device__ __forceinline__ void store_partials(const unsigned long long (&c)[C_N
     if (threadIdx.x < C_N + 2) {
         unsigned long long v = 0;
         for (int w = 0; w < NWAVES; ++w) v += part[w][threadIdx.x];
-        partials[(size_t)blockIdx.x * (C_N + 2) + threadIdx.x] = v;
+        if (v) atomicAdd(&partials[(size_t)(blockIdx.x % kPartRows) * (C_N + 2) + threadIdx.x], v);
     }
 }
 
@@ -671,7 +677,6 @@ __global__ __launch_bounds__(64 * kFusedWaves, kFusedMinWaves) void mc_fused_ker
 // the residual is nonzero, convergence fails, both iteration counts).  withX / withZ were counted by
 // mc_fused_kernel.
 constexpr int kSurvWaves = 4;
-constexpr int kReduceGroups = 16;  // its first workgroups also add mc_fused_kernel's partial sums
 
 // One lane of an I-P check group (CheckLogicalError, Quantum_LDPC_Code.h:126-142, as
 // logical_from_columns): word k of the XOR of the I-P columns at the set bits of the residual res[0, nw)
@@ -722,18 +727,11 @@ __global__ __launch_bounds__(64 * kSurvWaves) void mc_survivor_kernel(const Fuse
     __shared__ uint32_t region[64 * kSurvWaves * RS];
     __shared__ unsigned long long part[kSurvWaves][C_N + 2];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    if (blockIdx.x < kReduceGroups) {  // mc_fused_kernel's per-workgroup partial sums into the counters
-        const int R = (int)gridDim.x < kReduceGroups ? (int)gridDim.x : kReduceGroups;
-        unsigned long long v[C_N + 2] = {};
-        for (long long w = blockIdx.x + (long long)R * threadIdx.x; w < a.nparts; w += (long long)R * blockDim.x)
-#pragma unroll
-            for (int q = 0; q < C_N + 2; ++q) v[q] += a.partials[w * (C_N + 2) + q];
-#pragma unroll
-        for (int q = 0; q < C_N + 2; ++q)
-#pragma unroll
-            for (int o = 32; o >= 1; o >>= 1) v[q] += __shfl_xor(v[q], o);
-        flush_counters<kSurvWaves>(v, part, a.counters);
-        __syncthreads();  // part is used again below
+    if (blockIdx.x == 0 && threadIdx.x < C_N + 2) {  // mc_fused_kernel's partial-sum rows into the counters
+        unsigned long long v = 0;
+#pragma unroll 16
+        for (int r = 0; r < kPartRows; ++r) v += a.partials[r * (C_N + 2) + threadIdx.x];
+        if (v) atomicAdd(&a.counters[threadIdx.x], v);
     }
     const long long cnt = a.counts[2 * kCountStride];
     if ((long long)blockIdx.x * blockDim.x >= cnt) return;  // workgroup-uniform: no survivor for this one
@@ -891,9 +889,11 @@ static bool fused_fns(const Code& c, FusedFns& f)
     return true;
 }
 
-// workgroups of the fused kernel for a batch of B samples (rows of the partials workspace); the
+// workgroups of the fused kernel for a batch of B samples; the
 // list lengths' words (counts) span mc_fused_count_words()
 long long mc_fused_parts(long long B) { return (B + 64LL * kFusedWaves - 1) / (64LL * kFusedWaves); }
+// rows of the partials workspace, zeroed before every fused kernel
+int mc_fused_part_rows() { return kPartRows; }
 int mc_fused_count_words() { return 2 * kCountStride + 1; }
 int mc_fused_count_stride() { return kCountStride; }
 
@@ -947,15 +947,17 @@ int launch_mc_fused(const Code& c, uint64_t seed, uint64_t start, long long B, f
 // Zeroes n 64-bit words on the stream (the fused pipeline's counters and list lengths before a batch):
 // a one-workgroup kernel of this library instead of hipMemsetAsync, whose fill launch left ~4 us of
 // idle GPU before the next kernel (profiles/r06/ab/cmp_zero_kernel.txt)
-__global__ __launch_bounds__(256) void zero_words_kernel(unsigned long long* __restrict__ w, int n)
+__global__ __launch_bounds__(256) void zero_words_kernel(unsigned long long* __restrict__ w, int n,
+                                                         unsigned long long* __restrict__ w2, int n2)
 {
     for (int i = threadIdx.x; i < n; i += blockDim.x) w[i] = 0ull;
+    for (int i = threadIdx.x; i < n2; i += blockDim.x) w2[i] = 0ull;
 }
 
-int launch_zero_words(unsigned long long* w, int n, hipStream_t st)
+int launch_zero_words(unsigned long long* w, int n, hipStream_t st, unsigned long long* w2, int n2)
 {
-    if (n <= 0) return QEC_OK;
-    hipLaunchKernelGGL(zero_words_kernel, dim3(1), dim3(256), 0, st, w, n);
+    if (n <= 0 && n2 <= 0) return QEC_OK;
+    hipLaunchKernelGGL(zero_words_kernel, dim3(1), dim3(256), 0, st, w, n, w2, n2);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(QEC_ERR_HIP, std::string("zero words launch: ") + hipGetErrorString(e));
     return QEC_OK;
